@@ -1,0 +1,150 @@
+/*
+ * pt_capi.h — C-ABI of the MI355X path-tracing library (libpt_hip.so).
+ *
+ * Drop-in boundary for the reference's per-pixel radiance loop
+ * (/root/reference/main.py:186-271).  The reference has no native FFI: its
+ * only operator seam is two Python callables handed to
+ * multiprocessing.Pool.apply_async —
+ *     intersect_objects(ray, objects, light_obj)      main.py:83, :200-201
+ *     compute_color(scene, obj, point, normal)        main.py:142, :218-219
+ * — driven by the spp x bounce loop of main.py:186-271.  This header replaces
+ * that whole loop (pt_render*), and exposes the two callables as batched
+ * entry points (pt_intersect_objects, pt_compute_color) so a caller can swap
+ * them in one at a time.  Python binds it with ctypes
+ * (pathtracerpython_amd/_native.py); INTEGRATION.md shows the binding.
+ *
+ * Conventions: plain C types only.  Return 0 on success, a negative
+ * PT_E* code on failure; pt_last_error() gives a thread-local message.  Input
+ * arrays are caller-owned and read-only; the library copies what it needs to
+ * device memory at pt_scene_create.  Output buffers are caller-allocated.
+ * A pt_scene handle is not re-entrant (one call at a time per handle).
+ */
+#ifndef PT_CAPI_H
+#define PT_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_API_VERSION 1
+
+/* error codes */
+#define PT_OK 0
+#define PT_EINVAL (-1)     /* bad argument (shape, range, null pointer) */
+#define PT_EHIP (-2)       /* HIP runtime error */
+#define PT_ENOMEM (-3)     /* device or host allocation failed */
+#define PT_ENODEV (-4)     /* no usable gfx950 device */
+
+/* pt_render flags */
+#define PT_FLAG_RR (1u << 0)           /* Russian roulette (build extension) */
+#define PT_FLAG_FORCE_F64 (1u << 1)    /* send every intersection test to the
+                                          f64 evaluator (self-check mode) */
+#define PT_FLAG_COUNT (1u << 2)        /* fill pt_stats counters (slower) */
+
+/*
+ * Flattened scene, as produced by scene_reader.Scene
+ * (/root/reference/scene_reader.py:107-188).  Triangles are ordered exactly
+ * as the reference iterates them in intersect_objects (main.py:91-96):
+ * every object's triangles in scene order, then the light's triangles.
+ */
+typedef struct pt_scene_desc {
+    int32_t n_tri;           /* all triangles (objects + light)               */
+    int32_t n_obj_tri;       /* leading triangles that belong to objects      */
+    int32_t n_obj;           /* objects (materials); light has index n_obj    */
+    int32_t reserved;
+    const double* tri_v;     /* [n_tri][3][3] vertices v1,v2,v3 as read       */
+    const double* tri_n;     /* [n_tri][3] Obj.normals (scene_reader.py:5-8)  */
+    const double* tri_area;  /* [n_tri]    Obj.areas  (vector.py:164-165)     */
+    const int32_t* tri_obj;  /* [n_tri] object index; light triangles: n_obj  */
+    const double* mat;       /* [n_obj][8] red green blue ka kd ks kt n       */
+    double eye[3];           /* Scene.eye       scene_reader.py:151-152       */
+    double ortho[4];         /* Scene.ortho     x0 y0 x1 y1                   */
+    double ambient;          /* Scene.ambient                                 */
+    double light_rgb[3];     /* Scene.light_color                             */
+} pt_scene_desc;
+
+/* Render parameters.  Pixel k = ix*height + iy is the reference's list order
+ * (utils.py:64-69).  Rows: a launch renders the image rows iy with
+ * row_begin <= iy < row_end and iy % row_step == row_phase, which covers
+ * contiguous bands (row_step 1) and the interleaved bands used for
+ * multi-GPU balance.  Output: image orientation, float32
+ * out[(height-1-iy)][ix][3] restricted to the launched rows, packed in
+ * launch order (see pt_band_rows).  Values are the averaged radiance before
+ * make_image's min-max normalisation (main.py:274-280).                    */
+typedef struct pt_render_params {
+    int32_t width, height;
+    int32_t spp;             /* main.py -r                                     */
+    int32_t bounces;         /* main.py -b                                     */
+    uint64_t seed;           /* RNG key (SDL `seed`, unused by the reference) */
+    uint32_t flags;          /* PT_FLAG_*                                      */
+    int32_t rr_depth;        /* first bounce that may be terminated by RR     */
+    int32_t row_begin, row_end, row_step, row_phase;
+    int32_t sample_begin;    /* first sample index (spp-split renders)        */
+    int32_t reserved;
+} pt_render_params;
+
+/* Work counters (PT_FLAG_COUNT); reference-semantics test counts are those
+ * the reference loop would execute (shadow rays stop at the first occluding
+ * object, main.py:42-55).                                                   */
+typedef struct pt_stats {
+    uint64_t closest_tests;   /* intersect calls of intersect_objects        */
+    uint64_t shadow_tests;    /* intersect calls of compute_shadow_rays      */
+    uint64_t ray_bounces;     /* non-None rays traced                        */
+    uint64_t shading_points;  /* compute_color calls                         */
+    uint64_t light_hits;
+    uint64_t escapes;
+    uint64_t f64_fallbacks;   /* tests re-evaluated in f64 by the filter     */
+    uint64_t reserved;
+} pt_stats;
+
+typedef struct pt_scene pt_scene;
+
+int pt_api_version(void);
+const char* pt_last_error(void);
+
+/* number of HIP devices visible to the library */
+int pt_device_count(int32_t* count);
+
+/* Upload a scene to the current HIP device.  Replaces Scene(path)'s role as
+ * the thing the workers receive by pickle (main.py:201, :219). */
+int pt_scene_create(const pt_scene_desc* desc, pt_scene** out);
+void pt_scene_destroy(pt_scene* scene);
+
+/* Number of rows a launch with these params renders. */
+int pt_band_rows(const pt_render_params* p, int32_t* rows);
+
+/* Whole loop main.py:186-280 for the selected rows.  out_rgb_dev is a DEVICE
+ * pointer (float32, rows*width*3), written on `stream` (a hipStream_t, or
+ * NULL for the null stream).  Asynchronous; pt_last_kernel_ms() reads the
+ * HIP-event time of the most recent launch after the stream has synced. */
+int pt_render_device(pt_scene* scene, const pt_render_params* p,
+                     float* out_rgb_dev, void* stream, pt_stats* stats);
+
+/* Same, synchronous, with a host output buffer (rows*width*3 float32). */
+int pt_render(pt_scene* scene, const pt_render_params* p, float* out_rgb_host,
+              pt_stats* stats);
+
+/* Kernel time (ms) of the last pt_render_device launch on this handle. */
+int pt_last_kernel_ms(pt_scene* scene, float* ms);
+
+/* Batched replacement of intersect_objects (main.py:83-122).
+ * rays: [n][6] f64 (origin, direction — direction need not be normalised).
+ * out_tri [n]: closest triangle index or -1 (None); out_p [n][3]: hit point.
+ * The light flag of the reference is out_tri >= n_obj_tri. */
+int pt_intersect_objects(pt_scene* scene, const double* rays, int64_t n,
+                         int32_t* out_tri, double* out_p);
+
+/* Batched replacement of compute_color (main.py:142-145 + :23-80) with the
+ * 12 light-sampling uniforms given explicitly per point (slots 0..11).
+ * obj [n]: object index; point [n][3]; normal [n][3]; u [n][12];
+ * out_rgb [n][3] f64. */
+int pt_compute_color(pt_scene* scene, const int32_t* obj, const double* point,
+                     const double* normal, const double* u, int64_t n,
+                     double* out_rgb);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_CAPI_H */
