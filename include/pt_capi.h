@@ -95,8 +95,8 @@ typedef struct pt_stats {
     uint64_t shading_points;  /* compute_color calls                         */
     uint64_t light_hits;
     uint64_t escapes;
-    uint64_t f64_fallbacks;   /* tests re-evaluated in f64 by the filter     */
-    uint64_t reserved;
+    uint64_t f64_fallbacks;   /* single tests re-evaluated in f64 (filter)   */
+    uint64_t f64_rescans;     /* closest-hit queries re-run fully in f64     */
 } pt_stats;
 
 typedef struct pt_scene pt_scene;

@@ -42,11 +42,10 @@ class PtRenderParams(C.Structure):
 class PtStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "closest_tests", "shadow_tests", "ray_bounces", "shading_points",
-        "light_hits", "escapes", "f64_fallbacks", "reserved")]
+        "light_hits", "escapes", "f64_fallbacks", "f64_rescans")]
 
     def as_dict(self):
-        return {n: int(getattr(self, n)) for n, _ in self._fields_
-                if n != "reserved"}
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
 def make_params(width, height, spp, bounces, seed, flags=0, rr_depth=3,

@@ -1,0 +1,82 @@
+"""ctypes binding of libpt_hip.so (include/pt_capi.h).
+
+The HIP library is the only implementation of the hot path: there is no CPU
+fallback.  If the library is missing or no gfx950 device is visible, calls
+raise `NativeError` — loudly, never silently.
+"""
+import ctypes as C
+import os
+
+from ._abi import PtRenderParams, PtSceneDesc, PtStats
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PT_HIP_LIB", os.path.join(HERE, "_lib", "libpt_hip.so"))
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _bind(lib):
+    vp = C.c_void_p
+    dp = C.POINTER(C.c_double)
+    ip = C.POINTER(C.c_int32)
+    sig = {
+        "pt_api_version": ([], C.c_int),
+        "pt_last_error": ([], C.c_char_p),
+        "pt_device_count": ([ip], C.c_int),
+        "pt_scene_create": ([C.POINTER(PtSceneDesc), C.POINTER(vp)], C.c_int),
+        "pt_scene_destroy": ([vp], None),
+        "pt_band_rows": ([C.POINTER(PtRenderParams), ip], C.c_int),
+        "pt_render_device": ([vp, C.POINTER(PtRenderParams), vp, vp, C.POINTER(PtStats)], C.c_int),
+        "pt_render": ([vp, C.POINTER(PtRenderParams), C.POINTER(C.c_float), C.POINTER(PtStats)], C.c_int),
+        "pt_last_kernel_ms": ([vp, C.POINTER(C.c_float)], C.c_int),
+        "pt_intersect_objects": ([vp, dp, C.c_int64, ip, dp], C.c_int),
+        "pt_compute_color": ([vp, ip, dp, dp, dp, C.c_int64, dp], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+EXPORTS = ("pt_api_version", "pt_last_error", "pt_device_count", "pt_scene_create",
+           "pt_scene_destroy", "pt_band_rows", "pt_render_device", "pt_render",
+           "pt_last_kernel_ms", "pt_intersect_objects", "pt_compute_color")
+
+
+def lib():
+    """Load libpt_hip.so once.  torch (if present) is imported first so the
+    library binds to the same HIP runtime instance torch uses."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"{LIB_PATH} not found: build it with `python __graft_entry__.py build` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    try:
+        import torch  # noqa: F401  (shares libamdhip64 with torch)
+    except Exception:
+        pass
+    _lib = _bind(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def last_error():
+    msg = lib().pt_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc, what):
+    if rc != 0:
+        raise NativeError(f"{what} failed ({rc}): {last_error()}")
+
+
+def device_count():
+    n = C.c_int32(0)
+    check(lib().pt_device_count(C.byref(n)), "pt_device_count")
+    return n.value

@@ -1,0 +1,267 @@
+// pt_core.h — numerics of the hot path, shared by the gfx950 kernels and the
+// host-side self-test (compiled as __host__ __device__).
+//
+// Reference semantics reproduced here (thiagoald/pathtracerpython):
+//   intersect(ray, triangle)        utils.py:98-147   -> eval64()
+//   in_triangle(pt, triangle)       utils.py:72-91    -> eval64()
+//   intersect_objects               main.py:83-122    -> closest_* (pt_hip.hip)
+//   compute_shadow_rays             main.py:23-73     -> nee() (pt_hip.hip)
+//   pick_random_triangle            utils.py:28-39    -> pick_light()
+//   sample_random_pt / bary coords  utils.py:21-46    -> light_point()
+//   rotate(axis=(0,1,0), ...)       main.py:148-162   -> TriS::R (host precompute)
+//   uniform(a, b)                   main.py:16        -> keyed Philox (philox())
+//
+// Precision design: every test is first run in f32 through a
+// *filter* that returns a decision only when it is certain under a rigorous
+// per-triangle error bound; otherwise the test is re-evaluated in f64 with
+// the reference's own formula.  All path state (origins, directions,
+// throughput, colours) is f64.  Hence results track the f64 reference to
+// ~1e-15 instead of inheriting f32 hit/miss flips.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#define PT_HD __host__ __device__ __forceinline__
+
+namespace pt {
+
+constexpr double kZero = 1e-5;        // main.py:20, utils.py:18
+constexpr double kTau = 6.28;         // main.py:19
+constexpr int kLightSamples = 3;      // main.py:23
+constexpr float kU = 5.9604645e-08f;  // 2^-24, f32 unit roundoff
+
+// |t| thresholds equivalent to squared distance 1e-5, with slack
+constexpr float kTzLo = 0.0031622745f;   // sqrt(1e-5) * (1 - 1e-6)
+constexpr float kTzHi = 0.0031622809f;   // sqrt(1e-5) * (1 + 1e-6)
+
+// ------------------------------------------------------------- records --
+// f32 filter record (80 B, one s_load_dwordx16 + one dwordx4).  Coordinates
+// are relative to SceneK::center.  Forms (x = origin, d = unit direction):
+//   h(x) = n.x + cn      signed distance to the plane (n = reference v_plane)
+//   b(x) = gb.x + cb     barycentric weight of v2   (affine, plane-invariant)
+//   c(x) = gc.x + cc     barycentric weight of v3
+// Error constants (see host prepare, pt_scene.cpp):
+//   eh, eq : abs error of h(o) and q = n.d
+//   eo, ed : abs error of b(o)/c(o) and b(d)/c(d) (max of the two)
+//   g      : max(|gb|_1, |gc|_1)
+//   qlo,qhi: |q| below qlo is certainly <= 1e-5 (parallel reject), above qhi
+//            certainly > 1e-5
+//   grp    : coplanar group (host-verified in f64).  A line whose origin lies
+//            on a triangle of the same group meets this plane at |t| < 1e-3,
+//            i.e. squared distance < 1e-5: certainly not a usable hit.
+struct alignas(16) TriF {
+    float n[3], cn;
+    float gb[3], cb;
+    float gc[3], cc;
+    float eh, eq, eo, ed;
+    float g, qlo, qhi;
+    int32_t grp;
+};
+
+// f64 exact record: the reference's plane normal and edges (utils.py:109-111,
+// :78-80).  cvp = dot(vp, v1).
+struct alignas(16) TriD {
+    double vp[3], cvp;
+    double v1[3], v2[3], v3[3];
+    double e12[3], e23[3], e31[3];   // v1-v2, v2-v3, v3-v1
+    double pad;
+};
+
+// shading record: Obj.normals (scene_reader.py:5-8) and the rotate() matrix
+// for angle arccos(n_y) about +y (main.py:248-249); other entries are +-0.
+struct alignas(16) TriS {
+    double n[3];
+    double r00, r02, r11, r20, r22;
+};
+
+struct alignas(16) Mat {
+    double rgb[3], ka;
+    double kd, ks, kdks, nexp;   // kdks = kd + ks (main.py:240)
+    int32_t nint;                // nexp as an integer when it is one, else -1
+    int32_t pad[3];
+};
+
+struct SceneK {
+    const TriF* trif;
+    const TriD* trid;
+    const TriS* tris;
+    const int32_t* tri_obj;
+    const Mat* mat;
+    const int32_t* light_tri;   // [n_light] global triangle index
+    const double* light_cum;    // [n_light+1] running area sums (utils.py:31-35)
+    int32_t n_tri, n_obj_tri, n_obj, n_light;
+    double light_sum;
+    double eye[3];
+    double ortho[4];
+    double ambient;
+    double light_rgb[3];
+    double center[3];
+};
+
+// ------------------------------------------------------------------ RNG --
+// Philox4x32-10 (Salmon et al., SC'11), key = seed, counter =
+// (pixel, sample, bounce, slot>>2); see tests/golden/philox_ref.py.
+PT_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[1] = (uint32_t)p1;
+        c[3] = (uint32_t)p0;
+        c[0] = n0;
+        c[2] = n2;
+    }
+}
+
+PT_HD void rng_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce,
+                     uint32_t blk, uint32_t w[4]) {
+    w[0] = pixel; w[1] = sample; w[2] = bounce; w[3] = blk;
+    philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+PT_HD double u_of(uint32_t w) { return (double)(w >> 8) * (1.0 / 16777216.0); }
+
+// ------------------------------------------------------------- vectors --
+struct D3 { double x, y, z; };
+struct F3 { float x, y, z; };
+
+PT_HD D3 d3(double x, double y, double z) { D3 r; r.x = x; r.y = y; r.z = z; return r; }
+PT_HD D3 ld3(const double* p) { return d3(p[0], p[1], p[2]); }
+PT_HD D3 operator+(D3 a, D3 b) { return d3(a.x + b.x, a.y + b.y, a.z + b.z); }
+PT_HD D3 operator-(D3 a, D3 b) { return d3(a.x - b.x, a.y - b.y, a.z - b.z); }
+PT_HD D3 operator*(D3 a, double s) { return d3(a.x * s, a.y * s, a.z * s); }
+PT_HD double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PT_HD D3 cross(D3 a, D3 b) {   // np.cross component formulas
+    return d3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+// squared_dist(pt1, pt2), utils.py:48-49 (sum from 0, component order)
+PT_HD double squared_dist(D3 a, D3 b) {
+    const double dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+    return ((0.0 + dx * dx) + dy * dy) + dz * dz;
+}
+PT_HD D3 unit(D3 a) {   // v / np.linalg.norm(v), with one reciprocal
+    const double inv = 1.0 / sqrt(dot(a, a));
+    return a * inv;
+}
+PT_HD F3 to_f3(D3 a) { F3 r; r.x = (float)a.x; r.y = (float)a.y; r.z = (float)a.z; return r; }
+
+// -------------------------------------------------------- exact (f64) --
+// intersect(ray, triangle) of utils.py:98-147 + squared_dist to the origin.
+// dn: normalised direction (utils.py:110).  Returns hit, P, sqd = |P - o|^2.
+// in_triangle's normalisations are skipped: only the signs of c1.c2 and
+// c1.c3 matter, and a zero cross product gives 0 -> "outside", as the
+// reference's NaN does.
+PT_HD bool eval64(const TriD& T, D3 o, D3 dn, D3* P, double* sqd) {
+    const D3 vp = ld3(T.vp);
+    const double den = dot(dn, vp);
+    if (!(fabs(den) > kZero)) return false;
+    const double t = (T.cvp - dot(vp, o)) / dot(vp, dn);
+    const D3 p = o + dn * t;
+    const D3 c1 = cross(ld3(T.e12), p - ld3(T.v2));
+    const D3 c2 = cross(ld3(T.e23), p - ld3(T.v3));
+    const D3 c3 = cross(ld3(T.e31), p - ld3(T.v1));
+    *P = p;
+    *sqd = squared_dist(p, o);
+    return dot(c1, c2) > 0.0 && dot(c1, c3) > 0.0;
+}
+
+// --------------------------------------------------------- f32 filter --
+PT_HD float aff3(const float g[3], float c, F3 x) {
+    return fmaf(g[0], x.x, fmaf(g[1], x.y, fmaf(g[2], x.z, c)));
+}
+PT_HD float lin3(const float g[3], F3 x) {
+    return fmaf(g[0], x.x, fmaf(g[1], x.y, g[2] * x.z));
+}
+PT_HD float min3f(float a, float b, float c) { return fminf(a, fminf(b, c)); }
+
+PT_HD float rcpf(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);   // v_rcp_f32, 1 ulp; covered by eq/eh slack
+#else
+    return 1.0f / x;
+#endif
+}
+
+// Filter verdicts
+enum : int { kMiss = 0, kCand = 1, kAmb = 2 };
+
+// Origin-dependent parts of a test, shared by rays with the same origin.
+struct OriginF { float h, bo, co; };
+PT_HD OriginF origin_f(const TriF& T, F3 o) {
+    OriginF r;
+    r.h = aff3(T.n, T.cn, o);
+    r.bo = aff3(T.gb, T.cb, o);
+    r.co = aff3(T.gc, T.cc, o);
+    return r;
+}
+
+// Core classification.  Returns kMiss when the reference certainly reports
+// "no intersection usable in range", kCand when it certainly reports an
+// intersection inside the triangle with |t| in (lo, hi) (|t| interval
+// [t-dt, t+dt] returned), kAmb otherwise.  Range semantics:
+//   closest: valid iff sqd > 1e-5                 -> lo = kTz, hi = inf
+//   shadow : occluder iff 1e-5 <= sqd < |L - P|^2 -> lo = kTz, hi = tL
+PT_HD int classify(const TriF& T, const OriginF& O, F3 d, float hi_lo, float hi_hi,
+                   float* t_abs, float* t_err) {
+    const float q = lin3(T.n, d);
+    const float aq = fabsf(q);
+    if (aq < T.qlo) return kMiss;                       // certainly |dot| <= 1e-5
+    const bool par_amb = !(aq > T.qhi);
+    const float r = rcpf(q);
+    const float t = -O.h * r;
+    const float at = fabsf(t);
+    const float dt = fmaf(fmaf(at, T.eq, T.eh), fabsf(r), 8.0f * kU * at);
+    const float beta = fmaf(t, lin3(T.gb, d), O.bo);
+    const float gam = fmaf(t, lin3(T.gc, d), O.co);
+    const float alpha = (1.0f - beta) - gam;
+    // |beta_ref - beta| <= del2, |gamma_ref - gamma| <= del2,
+    // |alpha_ref - alpha| <= 2*del2 (alpha = 1 - beta - gamma, two roundings)
+    const float del2 = fmaf(T.g, dt, fmaf(at, T.ed, T.eo)) + 8.0f * kU;
+    // certainly outside: some weight certainly negative (miss whether or not
+    // the reference's parallel test fires)
+    if (min3f(beta, gam, alpha + del2) < -del2) return kMiss;
+    if (at + dt < kTzLo) return kMiss;                  // certainly |P - o|^2 < 1e-5
+    if (at - dt >= hi_hi) return kMiss;                 // certainly beyond the range
+    *t_abs = at;
+    *t_err = dt;
+    const bool inside = min3f(beta, gam, alpha - del2) > del2;
+    const bool in_range = (at - dt > kTzHi) && (at + dt < hi_lo);
+    return (!par_amb && inside && in_range) ? kCand : kAmb;
+}
+
+// ------------------------------------------------------ light sampling --
+// pick_random_triangle, utils.py:28-39: first i with cum[i] <= n < cum[i+1]
+PT_HD int pick_light(const SceneK& S, double u) {
+    const double n = 0.0 + (S.light_sum - 0.0) * u;
+    for (int i = 0; i < S.n_light; ++i)
+        if (S.light_cum[i] <= n && n < S.light_cum[i + 1]) return i;
+    return 0;   // unreachable for u < 1 (the reference would fail here)
+}
+
+// sample_random_pt with sample_bary_coords, utils.py:21-25, :42-46
+PT_HD D3 light_point(const TriD& T, double u1, double u2, double u3) {
+    const double inv = 1.0 / (((0.0 + u1) + u2) + u3);
+    const double a = u1 * inv, b = u2 * inv, c = u3 * inv;
+    return d3(a * T.v1[0] + b * T.v2[0] + c * T.v3[0],
+              a * T.v1[1] + b * T.v2[1] + c * T.v3[1],
+              a * T.v1[2] + b * T.v2[2] + c * T.v3[2]);
+}
+
+// ------------------------------------------------------------- bounce --
+PT_HD D3 rotate_y(const TriS& R, D3 v) {   // np.dot(rotation_matrix, v)
+    return d3(R.r00 * v.x + R.r02 * v.z, R.r11 * v.y, R.r20 * v.x + R.r22 * v.z);
+}
+
+PT_HD double pow_ref(double x, const Mat& m) {   // x ** n (numpy float power)
+    if (m.nint >= 0 && m.nint <= 16) {
+        double r = 1.0;
+        for (int i = 0; i < m.nint; ++i) r *= x;
+        return r;
+    }
+    return pow(x, m.nexp);
+}
+
+}  // namespace pt

@@ -1,0 +1,454 @@
+// pt_hip.hip — gfx950 kernels + C-ABI (include/pt_capi.h) of the MI355X path
+// tracer.  Replaces the reference's spp x bounce loop (main.py:186-280) and its
+// two Pool callables (intersect_objects main.py:83, compute_color main.py:142).
+//
+// Kernel geometry: one work-item per (pixel, sample-slice);
+// `split` adjacent lanes share a pixel and stride its samples, so the whole
+// pixel lives in one wave and is reduced with DPP/shuffles in a fixed order
+// (deterministic).  Triangles are read with uniform indices -> scalar loads
+// (s_load_dwordx16) from the 80-B f32 filter records; only rare ambiguous
+// tests touch the f64 records.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <mutex>
+#include <string>
+
+#include "pt_path.h"
+#include "pt_prepare.h"
+
+using namespace pt;
+
+// ------------------------------------------------------------- errors --
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIPCHK(expr)                                                              \
+    do {                                                                          \
+        hipError_t e_ = (expr);                                                   \
+        if (e_ != hipSuccess)                                                     \
+            return fail(PT_EHIP, std::string(#expr " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// ------------------------------------------------------------- kernels --
+struct RenderK {
+    int32_t W, H, spp, bounces;
+    uint64_t seed;
+    int32_t rr_depth;   // -1: off
+    int32_t first_row, row_step, n_rows;
+    int32_t sample_begin;
+    uint32_t split, split_log2;
+    uint32_t npix;
+};
+
+struct StatsDev { unsigned long long v[8]; };
+
+template <bool COUNT>
+__device__ __forceinline__ void flush_counters(const Counters& c, StatsDev* st) {
+    if (!COUNT) return;
+    uint32_t v[8] = {c.closest_tests, c.shadow_tests, c.ray_bounces, c.shading_points,
+                     c.light_hits, c.escapes, c.fallbacks, c.rescans};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t x = v[i];
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&st->v[i], (unsigned long long)x);
+    }
+}
+
+template <bool FORCE64, bool COUNT>
+__global__ __launch_bounds__(256) void k_render(SceneK S, RenderK R, float* __restrict__ out,
+                                                StatsDev* __restrict__ st) {
+    const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t pl = tid >> R.split_log2;
+    const uint32_t c = tid & (R.split - 1u);
+    const bool valid = pl < R.npix;
+    Counters cnt = {};
+    D3 acc = d3(0, 0, 0);
+    int32_t row_local = 0, ix = 0;
+    if (valid) {
+        row_local = (int32_t)(pl / (uint32_t)R.W);
+        ix = (int32_t)pl - row_local * R.W;
+        const int32_t iy = R.first_row + row_local * R.row_step;
+        // make_screen_pts / make_rays, utils.py:55-69
+        const D3 eye = ld3(S.eye);
+        const double x = linspace_at(S.ortho[0], S.ortho[2], R.W, ix);
+        const double y = linspace_at(S.ortho[1], S.ortho[3], R.H, iy);
+        const D3 d0 = d3(x - eye.x, y - eye.y, 0.0 - eye.z);
+        const int32_t ns = ((int32_t)c < R.spp) ? (R.spp - (int32_t)c + (int32_t)R.split - 1) / (int32_t)R.split : 0;
+        LaneJob J;
+        J.seed = R.seed;
+        J.pixel = (uint32_t)ix * (uint32_t)R.H + (uint32_t)iy;
+        J.sample0 = R.sample_begin + (int32_t)c;
+        J.sample_stride = (int32_t)R.split;
+        J.n_samples = ns;
+        J.bounces = R.bounces;
+        J.rr_depth = R.rr_depth;
+        D3 P0 = d3(0, 0, 0);
+        int tri0 = -1;
+        if (ns > 0 && R.bounces > 0) tri0 = closest<FORCE64, false>(S, eye, d0, -1, &P0, &cnt);
+        acc = render_lane<FORCE64, COUNT>(S, J, eye, d0, tri0, P0, &cnt);
+    }
+    for (uint32_t m = 1; m < R.split; m <<= 1) {
+        acc.x += __shfl_xor(acc.x, (int)m);
+        acc.y += __shfl_xor(acc.y, (int)m);
+        acc.z += __shfl_xor(acc.z, (int)m);
+    }
+    if (valid && c == 0) {
+        const double inv = (double)R.spp;
+        float* o = out + ((size_t)(R.n_rows - 1 - row_local) * (size_t)R.W + (size_t)ix) * 3;
+        o[0] = (float)(acc.x / inv);
+        o[1] = (float)(acc.y / inv);
+        o[2] = (float)(acc.z / inv);
+    }
+    flush_counters<COUNT>(cnt, st);
+}
+
+__global__ __launch_bounds__(256) void k_intersect(SceneK S, const double* __restrict__ rays,
+                                                   int64_t n, float xb, int32_t* __restrict__ out_tri,
+                                                   double* __restrict__ out_p) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const D3 o = ld3(rays + 6 * i), d = ld3(rays + 6 * i + 3);
+    const F3 oc = to_f3(o - ld3(S.center));
+    const bool in_box = fabsf(oc.x) <= xb && fabsf(oc.y) <= xb && fabsf(oc.z) <= xb;
+    D3 P = d3(0, 0, 0);
+    Counters c;
+    const int t = in_box ? closest<false, false>(S, o, d, -1, &P, &c) : closest<true, false>(S, o, d, -1, &P, &c);
+    out_tri[i] = t;
+    out_p[3 * i] = P.x; out_p[3 * i + 1] = P.y; out_p[3 * i + 2] = P.z;
+}
+
+__global__ __launch_bounds__(256) void k_color(SceneK S, const int32_t* __restrict__ obj,
+                                               const double* __restrict__ point,
+                                               const double* __restrict__ normal,
+                                               const double* __restrict__ u, int64_t n, float xb,
+                                               double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const D3 P = ld3(point + 3 * i);
+    double uu[12];
+    for (int j = 0; j < 12; ++j) uu[j] = u[12 * i + j];
+    const F3 oc = to_f3(P - ld3(S.center));
+    const bool in_box = fabsf(oc.x) <= xb && fabsf(oc.y) <= xb && fabsf(oc.z) <= xb;
+    Counters c;
+    const D3 col = in_box ? nee<false, false>(S, P, ld3(normal + 3 * i), obj[i], -1, uu, &c)
+                          : nee<true, false>(S, P, ld3(normal + 3 * i), obj[i], -1, uu, &c);
+    out[3 * i] = col.x; out[3 * i + 1] = col.y; out[3 * i + 2] = col.z;
+}
+
+// ---------------------------------------------------------------- API --
+struct pt_scene {
+    int device = 0;
+    HostScene host;
+    SceneK dev{};
+    float xbound = 0.f;
+    void* blob = nullptr;          // all scene tables, one allocation
+    StatsDev* stats = nullptr;
+    float* out_dev = nullptr;      // pt_render's staging buffer
+    size_t out_cap = 0;
+    hipStream_t stream = nullptr;  // pt_render's own stream
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+};
+
+namespace {
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+float box_bound(const HostScene& H) {
+    // origins handed to the filter must lie in the box its constants assume;
+    // recompute X exactly as prepare_scene does (centre / half extent)
+    double X = 0.0;
+    const SceneK& K = H.k;
+    for (const TriD& T : H.trid) {
+        const double* vs[3] = {T.v1, T.v2, T.v3};
+        for (int v = 0; v < 3; ++v)
+            for (int i = 0; i < 3; ++i) X = std::max(X, fabs(vs[v][i] - K.center[i]));
+    }
+    for (int i = 0; i < 3; ++i) X = std::max(X, fabs(K.eye[i] - K.center[i]));
+    return (float)X;
+}
+}  // namespace
+
+template <typename T>
+static int dev_alloc_copy(T** d, const T* h, size_t n) {
+    HIPCHK(hipMalloc((void**)d, n * sizeof(T) + 16));
+    if (h) HIPCHK(hipMemcpy(*d, h, n * sizeof(T), hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+extern "C" {
+
+int pt_api_version(void) { return PT_API_VERSION; }
+
+const char* pt_last_error(void) { return g_err.c_str(); }
+
+int pt_device_count(int32_t* count) {
+    if (!count) return fail(PT_EINVAL, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return PT_OK;
+}
+
+void pt_scene_destroy(pt_scene* s) {
+    if (!s) return;
+    {
+        DeviceGuard g(s->device);
+        if (s->blob) (void)hipFree(s->blob);
+        if (s->stats) (void)hipFree(s->stats);
+        if (s->out_dev) (void)hipFree(s->out_dev);
+        if (s->ev0) (void)hipEventDestroy(s->ev0);
+        if (s->ev1) (void)hipEventDestroy(s->ev1);
+        if (s->stream) (void)hipStreamDestroy(s->stream);
+    }
+    delete s;
+}
+
+int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
+    if (!out) return fail(PT_EINVAL, "null output handle");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(PT_ENODEV, "no HIP device visible (the MI355X path needs a gfx950 GPU)");
+    pt_scene* s = new pt_scene();
+    std::string err = prepare_scene(desc, &s->host);
+    if (!err.empty()) { delete s; return fail(PT_EINVAL, err); }
+    if (hipGetDevice(&s->device) != hipSuccess) { delete s; return fail(PT_EHIP, "hipGetDevice failed"); }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, s->device) == hipSuccess &&
+        std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+        std::string arch = prop.gcnArchName;
+        delete s;
+        return fail(PT_ENODEV, "device is " + arch + ", this build targets gfx950 only");
+    }
+    HostScene& H = s->host;
+    const size_t sz[7] = {H.trif.size() * sizeof(TriF), H.trid.size() * sizeof(TriD),
+                          H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
+                          H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
+                          H.light_cum.size() * sizeof(double)};
+    const void* src[7] = {H.trif.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
+                          H.mat.data(), H.light_tri.data(), H.light_cum.data()};
+    size_t off[7], total = 0;
+    for (int i = 0; i < 7; ++i) { off[i] = total; total += align_up(sz[i]); }
+    int rc = PT_OK;
+    auto cleanup = [&](int code, const std::string& m) { pt_scene_destroy(s); return fail(code, m); };
+    if (hipMalloc(&s->blob, total) != hipSuccess) return cleanup(PT_ENOMEM, "hipMalloc scene tables");
+    for (int i = 0; i < 7; ++i)
+        if (hipMemcpy((char*)s->blob + off[i], src[i], sz[i], hipMemcpyHostToDevice) != hipSuccess)
+            return cleanup(PT_EHIP, "hipMemcpy scene tables");
+    if (hipMalloc((void**)&s->stats, sizeof(StatsDev)) != hipSuccess) return cleanup(PT_ENOMEM, "hipMalloc stats");
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)
+        return cleanup(PT_EHIP, "stream/event creation");
+    s->dev = H.k;
+    char* b = (char*)s->blob;
+    s->dev.trif = (const TriF*)(b + off[0]);
+    s->dev.trid = (const TriD*)(b + off[1]);
+    s->dev.tris = (const TriS*)(b + off[2]);
+    s->dev.tri_obj = (const int32_t*)(b + off[3]);
+    s->dev.mat = (const Mat*)(b + off[4]);
+    s->dev.light_tri = (const int32_t*)(b + off[5]);
+    s->dev.light_cum = (const double*)(b + off[6]);
+    s->xbound = box_bound(H);
+    *out = s;
+    return rc;
+}
+
+int pt_band_rows(const pt_render_params* p, int32_t* rows) {
+    if (!p || !rows) return fail(PT_EINVAL, "null argument");
+    int32_t first;
+    if (!band_layout(p, &first, rows)) return fail(PT_EINVAL, "bad row_step/row_phase");
+    return PT_OK;
+}
+
+static int validate(const pt_render_params* p) {
+    if (!p) return fail(PT_EINVAL, "null params");
+    if (p->width <= 0 || p->height <= 0) return fail(PT_EINVAL, "width/height must be > 0");
+    if ((int64_t)p->width * p->height > (int64_t)1 << 32) return fail(PT_EINVAL, "image too large for 32-bit pixel keys");
+    if (p->spp <= 0) return fail(PT_EINVAL, "spp must be > 0");
+    if (p->bounces < 0) return fail(PT_EINVAL, "bounces must be >= 0");
+    if (p->sample_begin < 0) return fail(PT_EINVAL, "sample_begin must be >= 0");
+    if (p->row_step <= 0 || p->row_phase < 0 || p->row_phase >= p->row_step)
+        return fail(PT_EINVAL, "need row_step > 0 and 0 <= row_phase < row_step");
+    return PT_OK;
+}
+
+static uint32_t choose_split(uint32_t npix, int32_t spp) {
+    static const long env = [] {
+        const char* e = getenv("PT_SPLIT");
+        return e ? strtol(e, nullptr, 10) : 0L;
+    }();
+    uint32_t cap = 64;
+    while (cap > 1 && (int32_t)cap > spp) cap >>= 1;
+    if (env > 0) {
+        uint32_t s = 1;
+        while (s * 2 <= (uint32_t)env && s * 2 <= cap) s *= 2;
+        return s;
+    }
+    uint32_t s = 1;
+    const uint64_t target = (uint64_t)1 << 20;   // ~16k waves: 2 rounds of 8 waves x 256 CUs x 4
+    while (s < cap && (uint64_t)npix * s * 2 <= target) s *= 2;
+    return s;
+}
+
+int pt_render_device(pt_scene* s, const pt_render_params* p, float* out_dev, void* stream,
+                     pt_stats* stats) {
+    if (!s) return fail(PT_EINVAL, "null scene");
+    int rc = validate(p);
+    if (rc) return rc;
+    int32_t first = 0, rows = 0;
+    band_layout(p, &first, &rows);
+    if (rows == 0) return PT_OK;
+    if (!out_dev) return fail(PT_EINVAL, "null output");
+    DeviceGuard g(s->device);
+    hipStream_t st = (hipStream_t)stream;
+    RenderK R;
+    R.W = p->width; R.H = p->height; R.spp = p->spp; R.bounces = p->bounces;
+    R.seed = p->seed;
+    R.rr_depth = (p->flags & PT_FLAG_RR) ? std::max(0, p->rr_depth) : -1;
+    R.first_row = first; R.row_step = p->row_step; R.n_rows = rows;
+    R.sample_begin = p->sample_begin;
+    R.npix = (uint32_t)rows * (uint32_t)p->width;
+    R.split = choose_split(R.npix, p->spp);
+    R.split_log2 = 0;
+    while ((1u << R.split_log2) < R.split) ++R.split_log2;
+    const uint64_t threads = (uint64_t)R.npix * R.split;
+    const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+    const bool count = (p->flags & PT_FLAG_COUNT) != 0;
+    const bool f64 = (p->flags & PT_FLAG_FORCE_F64) != 0;
+    if (count) HIPCHK(hipMemsetAsync(s->stats, 0, sizeof(StatsDev), st));
+    HIPCHK(hipEventRecord(s->ev0, st));
+    if (f64) {
+        if (count) hipLaunchKernelGGL((k_render<true, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+        else hipLaunchKernelGGL((k_render<true, false>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+    } else {
+        if (count) hipLaunchKernelGGL((k_render<false, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+        else hipLaunchKernelGGL((k_render<false, false>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(s->ev1, st));
+    s->timed = true;
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        if (count) {
+            StatsDev h;
+            HIPCHK(hipMemcpyAsync(&h, s->stats, sizeof(h), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            stats->closest_tests = h.v[0];
+            stats->shadow_tests = h.v[1];
+            stats->ray_bounces = h.v[2];
+            stats->shading_points = h.v[3];
+            stats->light_hits = h.v[4];
+            stats->escapes = h.v[5];
+            stats->f64_fallbacks = h.v[6];
+            stats->f64_rescans = h.v[7];
+        }
+    }
+    return PT_OK;
+}
+
+int pt_render(pt_scene* s, const pt_render_params* p, float* out_host, pt_stats* stats) {
+    if (!s) return fail(PT_EINVAL, "null scene");
+    int rc = validate(p);
+    if (rc) return rc;
+    int32_t first = 0, rows = 0;
+    band_layout(p, &first, &rows);
+    if (rows == 0) return PT_OK;
+    if (!out_host) return fail(PT_EINVAL, "null output");
+    DeviceGuard g(s->device);
+    const size_t bytes = (size_t)rows * p->width * 3 * sizeof(float);
+    if (bytes > s->out_cap) {
+        if (s->out_dev) (void)hipFree(s->out_dev);
+        s->out_dev = nullptr;
+        s->out_cap = 0;
+        HIPCHK(hipMalloc((void**)&s->out_dev, bytes));
+        s->out_cap = bytes;
+    }
+    rc = pt_render_device(s, p, s->out_dev, s->stream, stats);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(out_host, s->out_dev, bytes, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return PT_OK;
+}
+
+int pt_last_kernel_ms(pt_scene* s, float* ms) {
+    if (!s || !ms) return fail(PT_EINVAL, "null argument");
+    if (!s->timed) return fail(PT_EINVAL, "no launch recorded yet");
+    DeviceGuard g(s->device);
+    HIPCHK(hipEventSynchronize(s->ev1));
+    HIPCHK(hipEventElapsedTime(ms, s->ev0, s->ev1));
+    return PT_OK;
+}
+
+int pt_intersect_objects(pt_scene* s, const double* rays, int64_t n, int32_t* out_tri,
+                         double* out_p) {
+    if (!s || (n > 0 && (!rays || !out_tri || !out_p))) return fail(PT_EINVAL, "null argument");
+    if (n <= 0) return PT_OK;
+    DeviceGuard g(s->device);
+    double *d_rays = nullptr, *d_p = nullptr;
+    int32_t* d_tri = nullptr;
+    int rc = dev_alloc_copy(&d_rays, rays, (size_t)n * 6);
+    if (!rc) rc = dev_alloc_copy(&d_p, (const double*)nullptr, (size_t)n * 3);
+    if (!rc) rc = dev_alloc_copy(&d_tri, (const int32_t*)nullptr, (size_t)n);
+    if (!rc) {
+        hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s->stream,
+                           s->dev, d_rays, n, s->xbound, d_tri, d_p);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+        if (e == hipSuccess) e = hipMemcpy(out_tri, d_tri, n * sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(out_p, d_p, n * 3 * sizeof(double), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(PT_EHIP, std::string("k_intersect: ") + hipGetErrorString(e));
+    }
+    if (d_rays) (void)hipFree(d_rays);
+    if (d_p) (void)hipFree(d_p);
+    if (d_tri) (void)hipFree(d_tri);
+    return rc;
+}
+
+int pt_compute_color(pt_scene* s, const int32_t* obj, const double* point, const double* normal,
+                     const double* u, int64_t n, double* out_rgb) {
+    if (!s || (n > 0 && (!obj || !point || !normal || !u || !out_rgb)))
+        return fail(PT_EINVAL, "null argument");
+    if (n <= 0) return PT_OK;
+    for (int64_t i = 0; i < n; ++i)
+        if (obj[i] < 0 || obj[i] >= s->host.k.n_obj) return fail(PT_EINVAL, "object index out of range");
+    DeviceGuard g(s->device);
+    int32_t* d_obj = nullptr;
+    double *d_pt = nullptr, *d_n = nullptr, *d_u = nullptr, *d_out = nullptr;
+    int rc = dev_alloc_copy(&d_obj, obj, (size_t)n);
+    if (!rc) rc = dev_alloc_copy(&d_pt, point, (size_t)n * 3);
+    if (!rc) rc = dev_alloc_copy(&d_n, normal, (size_t)n * 3);
+    if (!rc) rc = dev_alloc_copy(&d_u, u, (size_t)n * 12);
+    if (!rc) rc = dev_alloc_copy(&d_out, (const double*)nullptr, (size_t)n * 3);
+    if (!rc) {
+        hipLaunchKernelGGL(k_color, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s->stream,
+                           s->dev, d_obj, d_pt, d_n, d_u, n, s->xbound, d_out);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+        if (e == hipSuccess) e = hipMemcpy(out_rgb, d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(PT_EHIP, std::string("k_color: ") + hipGetErrorString(e));
+    }
+    for (void* p : {(void*)d_obj, (void*)d_pt, (void*)d_n, (void*)d_u, (void*)d_out})
+        if (p) (void)hipFree(p);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,253 @@
+// pt_prepare.h — host-side scene preparation: pt_scene_desc (include/pt_capi.h)
+// -> the device records of pt_core.h, including the f32 filter's rigorous
+// error constants.  Host-only C++.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pt_capi.h"
+#include "pt_core.h"
+
+namespace pt {
+
+struct HostScene {
+    std::vector<TriF> trif;
+    std::vector<TriD> trid;
+    std::vector<TriS> tris;
+    std::vector<int32_t> tri_obj;
+    std::vector<Mat> mat;
+    std::vector<int32_t> light_tri;
+    std::vector<double> light_cum;
+    SceneK k{};   // pointers unset; constants filled
+};
+
+inline D3 tri_vertex(const pt_scene_desc* d, int t, int v) {
+    return ld3(d->tri_v + 9 * t + 3 * v);
+}
+
+// rotate((0,1,0), arccos(n_y), .) matrix, main.py:148-162 literal formula
+inline void rotation_for_normal(const double* n, TriS* R) {
+    const double angle = acos(0.0 * n[0] + 1.0 * n[1] + 0.0 * n[2]);
+    const double a = cos(angle / 2.0), sn = sin(angle / 2.0);
+    const double b = -0.0 * sn, c = -1.0 * sn, dd = -0.0 * sn;
+    const double aa = a * a, bb = b * b, cc = c * c, d2 = dd * dd;
+    const double ac = a * c, bd = b * dd;
+    R->r00 = aa + bb - cc - d2;
+    R->r02 = 2 * (bd - ac);
+    R->r11 = aa + cc - bb - d2;
+    R->r20 = 2 * (bd + ac);
+    R->r22 = aa + d2 - bb - cc;
+}
+
+inline float f32_up(double x) {   // round to f32, never below x (x >= 0)
+    float f = (float)x;
+    if ((double)f < x) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+// Returns "" on success, else an error message.
+inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
+    if (!d) return "null scene descriptor";
+    if (d->n_tri <= 0 || d->n_obj_tri < 0 || d->n_obj_tri >= d->n_tri)
+        return "need 0 <= n_obj_tri < n_tri (the light must have triangles)";
+    if (d->n_obj <= 0) return "need at least one object";
+    if (!d->tri_v || !d->tri_n || !d->tri_area || !d->tri_obj || !d->mat)
+        return "null array in scene descriptor";
+    const int T = d->n_tri;
+    for (int t = 0; t < T; ++t) {
+        const int o = d->tri_obj[t];
+        if (t < d->n_obj_tri ? (o < 0 || o >= d->n_obj) : (o != d->n_obj))
+            return "tri_obj out of range (objects first, then light = n_obj)";
+    }
+    // scene box (vertices and eye) -> centre and half extent X
+    double lo[3], hi[3];
+    for (int i = 0; i < 3; ++i) lo[i] = hi[i] = d->eye[i];
+    for (int t = 0; t < T; ++t)
+        for (int v = 0; v < 3; ++v)
+            for (int i = 0; i < 3; ++i) {
+                const double x = d->tri_v[9 * t + 3 * v + i];
+                if (!isfinite(x)) return "non-finite vertex";
+                lo[i] = std::min(lo[i], x);
+                hi[i] = std::max(hi[i], x);
+            }
+    double C[3], X = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        C[i] = 0.5 * (lo[i] + hi[i]);
+        X = std::max(X, 0.5 * (hi[i] - lo[i]));
+    }
+    X = X * 1.001 + 1e-6;
+    const double u = 1.0 / 16777216.0;   // f32 unit roundoff
+
+    H->trif.assign(T, TriF{});
+    H->trid.assign(T, TriD{});
+    H->tris.assign(T, TriS{});
+    H->tri_obj.assign(d->tri_obj, d->tri_obj + T);
+    for (int t = 0; t < T; ++t) {
+        const D3 v1 = tri_vertex(d, t, 0), v2 = tri_vertex(d, t, 1), v3 = tri_vertex(d, t, 2);
+        TriD& E = H->trid[t];
+        // reference plane normal: normalize(cross(v1 - v2, v3 - v2)), utils.py:109-111
+        const D3 cr = cross(v1 - v2, v3 - v2);
+        const double cn = sqrt(dot(cr, cr));
+        const D3 vp = cr * (1.0 / cn);
+        E.vp[0] = cr.x / cn; E.vp[1] = cr.y / cn; E.vp[2] = cr.z / cn;  // v / norm(v)
+        E.cvp = E.vp[0] * v1.x + E.vp[1] * v1.y + E.vp[2] * v1.z;
+        const D3 e12 = v1 - v2, e23 = v2 - v3, e31 = v3 - v1;
+        const double* src[6] = {&v1.x, &v2.x, &v3.x, &e12.x, &e23.x, &e31.x};
+        double* dst[6] = {E.v1, E.v2, E.v3, E.e12, E.e23, E.e31};
+        for (int j = 0; j < 6; ++j) memcpy(dst[j], src[j], 3 * sizeof(double));
+        (void)vp;
+
+        TriS& R = H->tris[t];
+        memcpy(R.n, d->tri_n + 3 * t, 3 * sizeof(double));
+        rotation_for_normal(R.n, &R);
+
+        // f32 filter record in centred coordinates
+        TriF& F = H->trif[t];
+        const D3 Cd = d3(C[0], C[1], C[2]);
+        const D3 w1 = v1 - Cd, w2 = v2 - Cd, w3 = v3 - Cd;
+        const D3 e1 = w2 - w1, e2 = w3 - w1, N = cross(e1, e2);
+        const double NN = dot(N, N);
+        if (!(cn > 0.0) || !(NN > 0.0) || !isfinite(cn)) {
+            // degenerate: the reference's NaN normal fails |dot| > 1e-5 -> always miss
+            F.qlo = INFINITY;
+            F.qhi = INFINITY;
+            continue;
+        }
+        const D3 gb = cross(e2, N) * (1.0 / NN), gc = cross(N, e1) * (1.0 / NN);
+        const double cb = -dot(gb, w1), cc = -dot(gc, w1);
+        const double chn = -(E.vp[0] * w1.x + E.vp[1] * w1.y + E.vp[2] * w1.z);
+        F.n[0] = (float)E.vp[0]; F.n[1] = (float)E.vp[1]; F.n[2] = (float)E.vp[2];
+        F.cn = (float)chn;
+        F.gb[0] = (float)gb.x; F.gb[1] = (float)gb.y; F.gb[2] = (float)gb.z; F.cb = (float)cb;
+        F.gc[0] = (float)gc.x; F.gc[1] = (float)gc.y; F.gc[2] = (float)gc.z; F.cc = (float)cc;
+        // bounds: an f32 affine form g.x + c at |x_i| <= X, evaluated as an
+        // fma chain from rounded inputs, errs by <= 5u(|g|_1 X + |c|) (input
+        // and coefficient rounding 2u|g|_1 X + u|c|, three fmas 3u(...)); we
+        // use 8u and a further 1.25x for second-order terms.
+        auto l1 = [](double a, double b, double c) { return fabs(a) + fabs(b) + fabs(c); };
+        const double n1 = l1(F.n[0], F.n[1], F.n[2]) * (1 + 4 * u);
+        const double gb1 = l1(F.gb[0], F.gb[1], F.gb[2]) * (1 + 4 * u);
+        const double gc1 = l1(F.gc[0], F.gc[1], F.gc[2]) * (1 + 4 * u);
+        const double s = 1.25;
+        const double eh = s * 8 * u * (n1 * X + fabs(chn));
+        const double eq = s * 8 * u * n1;
+        const double eo = s * (8 * u * std::max(gb1 * X + fabs(cb), gc1 * X + fabs(cc))) + 4 * u;
+        const double ed = s * 8 * u * std::max(gb1, gc1);
+        F.eh = f32_up(eh);
+        F.eq = f32_up(eq);
+        F.eo = f32_up(eo);
+        F.ed = f32_up(ed);
+        F.g = f32_up(std::max(gb1, gc1) * (1 + 1e-3));
+        F.qlo = (float)((1e-5 - eq) * (1 - 1e-4));
+        if (!(F.qlo > 0.f)) F.qlo = 0.f;
+        F.qhi = f32_up((1e-5 + eq) * (1 + 1e-4));
+    }
+    // coplanar groups: triangle t joins the group of an earlier
+    // representative r when every vertex of t lies within 1e-12 of r's plane
+    // and every vertex of r within 1e-12 of t's plane (f64).  Members' planes
+    // then agree to ~1e-9 anywhere in the scene box, so a line from a hit
+    // point on one member meets another member's plane at
+    // |t| <= 1e-9 / |q| < 1e-4 (|q| > 1e-5, else the reference's parallel
+    // reject fires): squared distance < 1e-5, never a usable hit.  Candidate
+    // representatives are found by hashing the quantised plane; a missed
+    // grouping only costs speed, never correctness.
+    {
+        std::unordered_map<uint64_t, std::vector<int>> buckets;
+        int n_groups = 0;
+        std::vector<int> grp_of_rep;
+        auto plane_dist = [&](int plane_t, D3 x) {
+            const TriD& P = H->trid[plane_t];
+            return fabs(P.vp[0] * x.x + P.vp[1] * x.y + P.vp[2] * x.z - P.cvp);
+        };
+        for (int t = 0; t < T; ++t) {
+            TriF& F = H->trif[t];
+            F.grp = -2 - t;   // unique, never equal to an origin's -1
+            if (!(F.qlo < INFINITY)) continue;   // degenerate
+            const TriD& E = H->trid[t];
+            double k[4] = {E.vp[0], E.vp[1], E.vp[2], E.cvp};
+            // canonical sign: first significant normal component positive
+            const int lead = fabs(k[0]) > 1e-3 ? 0 : (fabs(k[1]) > 1e-3 ? 1 : 2);
+            if (k[lead] < 0) for (double& x : k) x = -x;
+            uint64_t key = 1469598103934665603ull;
+            for (int i = 0; i < 4; ++i) {
+                const int64_t qv = (int64_t)llround(k[i] * (i < 3 ? 1e5 : 1e3));
+                key = (key ^ (uint64_t)qv) * 1099511628211ull;
+            }
+            std::vector<int>& reps = buckets[key];
+            for (int r : reps) {
+                bool ok = true;
+                for (int v = 0; v < 3 && ok; ++v)
+                    ok = plane_dist(r, tri_vertex(d, t, v)) <= 1e-12 &&
+                         plane_dist(t, tri_vertex(d, r, v)) <= 1e-12;
+                if (ok) { F.grp = H->trif[r].grp; break; }
+            }
+            if (F.grp < 0) {
+                F.grp = n_groups++;
+                reps.push_back(t);
+            }
+        }
+    }
+    // materials
+    H->mat.assign(d->n_obj, Mat{});
+    for (int o = 0; o < d->n_obj; ++o) {
+        const double* m = d->mat + 8 * o;
+        Mat& M = H->mat[o];
+        M.rgb[0] = m[0]; M.rgb[1] = m[1]; M.rgb[2] = m[2];
+        M.ka = m[3]; M.kd = m[4]; M.ks = m[5];
+        M.kdks = m[4] + m[5];
+        M.nexp = m[7];
+        M.nint = (m[7] >= 0 && m[7] <= 16 && m[7] == floor(m[7])) ? (int32_t)m[7] : -1;
+    }
+    // light CDF: running sums from 0, utils.py:30-35
+    H->light_tri.clear();
+    H->light_cum.assign(1, 0.0);
+    double acc = 0.0;
+    for (int t = d->n_obj_tri; t < T; ++t) {
+        H->light_tri.push_back(t);
+        acc += d->tri_area[t];
+        H->light_cum.push_back(acc);
+    }
+    SceneK& K = H->k;
+    K.n_tri = T;
+    K.n_obj_tri = d->n_obj_tri;
+    K.n_obj = d->n_obj;
+    K.n_light = (int32_t)H->light_tri.size();
+    K.light_sum = acc;
+    for (int i = 0; i < 3; ++i) {
+        K.eye[i] = d->eye[i];
+        K.light_rgb[i] = d->light_rgb[i];
+        K.center[i] = C[i];
+    }
+    for (int i = 0; i < 4; ++i) K.ortho[i] = d->ortho[i];
+    K.ambient = d->ambient;
+    return "";
+}
+
+// host pointers (for the host-side check build)
+inline void bind_host(HostScene* H) {
+    H->k.trif = H->trif.data();
+    H->k.trid = H->trid.data();
+    H->k.tris = H->tris.data();
+    H->k.tri_obj = H->tri_obj.data();
+    H->k.mat = H->mat.data();
+    H->k.light_tri = H->light_tri.data();
+    H->k.light_cum = H->light_cum.data();
+}
+
+// first band row >= row_begin with iy % step == phase, and the band's row count
+inline bool band_layout(const pt_render_params* p, int32_t* first, int32_t* rows) {
+    if (p->row_step <= 0 || p->row_phase < 0 || p->row_phase >= p->row_step) return false;
+    const int32_t b = std::max(0, p->row_begin), e = std::min(p->height, p->row_end);
+    int32_t f = b + ((p->row_phase - b % p->row_step) + p->row_step) % p->row_step;
+    *first = f;
+    *rows = (f < e) ? (e - f + p->row_step - 1) / p->row_step : 0;
+    return true;
+}
+
+}  // namespace pt

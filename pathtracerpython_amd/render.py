@@ -1,0 +1,159 @@
+"""Host API of the MI355X path tracer: `render(scene, width, height, spp) ->
+framebuffer`, plus batched drop-ins for the reference's two Pool callables.
+
+The reference's render is the body of main() (main.py:165-293): for `-r` spp
+and `-b` bounces it traces every pixel of the SDL `size` and averages the
+samples (main.py:274-280).  Here that whole loop is one call into the HIP
+library (libpt_hip.so, include/pt_capi.h).  The RNG is the keyed Philox
+stream documented in tests/golden/philox_ref.py; the key defaults to the SDL
+`seed` (which the reference parses, scene_reader.py:169-170, but ignores).
+
+Framebuffers are float32, image orientation: fb[H-1-iy, ix] is the averaged
+radiance of the reference's pixel k = ix*H + iy (utils.py:64-69), before
+make_image's min-max normalisation.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _native
+from ._abi import PT_FLAG_COUNT, PT_FLAG_FORCE_F64, PT_FLAG_RR, PtStats, band_rows, make_params
+from .pack import pack_scene
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+class Renderer:
+    """A scene uploaded to the current HIP device (one `pt_scene` handle)."""
+
+    def __init__(self, scene):
+        self.scene = scene
+        self.packed = pack_scene(scene)
+        self._lib = _native.lib()
+        h = C.c_void_p()
+        _native.check(self._lib.pt_scene_create(C.byref(self.packed.desc), C.byref(h)),
+                      "pt_scene_create")
+        self._h = h
+
+    # ------------------------------------------------------------ render --
+    def params(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
+               rr_depth=3, force_f64=False, count=False, row_begin=0, row_end=None,
+               row_step=1, row_phase=0, sample_begin=0):
+        width = int(self.scene.width if width is None else width)
+        height = int(self.scene.height if height is None else height)
+        seed = self.scene.seed if seed is None else seed
+        seed = 0 if seed is None else int(seed)
+        flags = (PT_FLAG_RR if rr else 0) | (PT_FLAG_FORCE_F64 if force_f64 else 0) | \
+            (PT_FLAG_COUNT if count else 0)
+        return make_params(width, height, spp, bounces, seed, flags, rr_depth, row_begin,
+                           row_end, row_step, row_phase, sample_begin)
+
+    def band_rows(self, p):
+        n = C.c_int32(0)
+        _native.check(self._lib.pt_band_rows(C.byref(p), C.byref(n)), "pt_band_rows")
+        return n.value
+
+    def render_params(self, p, stats=False):
+        rows = self.band_rows(p)
+        out = np.zeros((rows, p.width, 3), dtype=np.float32)
+        st = PtStats()
+        _native.check(self._lib.pt_render(self._h, C.byref(p),
+                                          out.ctypes.data_as(C.POINTER(C.c_float)),
+                                          C.byref(st)), "pt_render")
+        return (out, st.as_dict()) if stats else out
+
+    def render(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
+               rr_depth=3, force_f64=False, stats=False, **band):
+        """Framebuffer (rows, W, 3) float32; rows = H for a full render."""
+        p = self.params(width, height, spp, bounces, seed, rr, rr_depth, force_f64,
+                        count=stats, **band)
+        return self.render_params(p, stats=stats)
+
+    def render_device(self, p, out_ptr, stream=None):
+        """Asynchronous render into a device buffer (e.g. a torch tensor's
+        data_ptr()) on a HIP stream handle (int) — used by the multi-GPU path."""
+        _native.check(self._lib.pt_render_device(self._h, C.byref(p), C.c_void_p(out_ptr),
+                                                 C.c_void_p(stream or 0), None),
+                      "pt_render_device")
+
+    def last_kernel_ms(self):
+        ms = C.c_float(0)
+        _native.check(self._lib.pt_last_kernel_ms(self._h, C.byref(ms)), "pt_last_kernel_ms")
+        return ms.value
+
+    # ------------------------------------------- batched Pool callables --
+    def intersect_objects(self, rays):
+        """Batched intersect_objects (main.py:83-122).  rays: (n, 6) origin,
+        direction.  Returns (tri (n,) int32, -1 = None; P (n, 3) f64).  The
+        reference's isItLight is tri >= packed.n_obj_tri."""
+        rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
+        n = rays.shape[0]
+        tri = np.zeros(n, dtype=np.int32)
+        P = np.zeros((n, 3), dtype=np.float64)
+        _native.check(self._lib.pt_intersect_objects(self._h, rays.ctypes.data_as(_dp), n,
+                                                     tri.ctypes.data_as(_ip),
+                                                     P.ctypes.data_as(_dp)),
+                      "pt_intersect_objects")
+        return tri, P
+
+    def compute_color(self, obj, point, normal, u):
+        """Batched compute_color (main.py:142-145) with the 12 light-sampling
+        uniforms of each point given explicitly (slots 0..11)."""
+        obj = np.ascontiguousarray(obj, dtype=np.int32).reshape(-1)
+        point = np.ascontiguousarray(point, dtype=np.float64).reshape(-1, 3)
+        normal = np.ascontiguousarray(normal, dtype=np.float64).reshape(-1, 3)
+        u = np.ascontiguousarray(u, dtype=np.float64).reshape(-1, 12)
+        n = obj.shape[0]
+        if not (point.shape[0] == normal.shape[0] == u.shape[0] == n):
+            raise ValueError("obj/point/normal/u must have the same length")
+        out = np.zeros((n, 3), dtype=np.float64)
+        _native.check(self._lib.pt_compute_color(self._h, obj.ctypes.data_as(_ip),
+                                                 point.ctypes.data_as(_dp),
+                                                 normal.ctypes.data_as(_dp),
+                                                 u.ctypes.data_as(_dp), n,
+                                                 out.ctypes.data_as(_dp)),
+                      "pt_compute_color")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.pt_scene_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render(scene, width=None, height=None, spp=1, bounces=1, seed=None, rr=False, rr_depth=3):
+    """main.py's render as a function: framebuffer (H, W, 3) float32."""
+    with Renderer(scene) as r:
+        return r.render(width, height, spp, bounces, seed, rr, rr_depth)
+
+
+def to_list_order(fb):
+    """Framebuffer (H, W, 3) -> (W*H, 3) in the reference's list order
+    k = ix*H + iy (the order of `colored_intersections`, main.py:177-183)."""
+    fb = np.asarray(fb)
+    H, W = fb.shape[:2]
+    return fb[::-1].transpose(1, 0, 2).reshape(W * H, 3)
+
+
+def from_list_order(colors, width, height):
+    """Inverse of to_list_order."""
+    c = np.asarray(colors).reshape(width, height, 3)
+    return c.transpose(1, 0, 2)[::-1]
+
+
+def band_row_indices(height, row_begin=0, row_end=None, row_step=1, row_phase=0):
+    """iy of each framebuffer row of a band render, top row first."""
+    return band_rows(height, row_begin, row_end, row_step, row_phase)[::-1]
