@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark: Mega path-samples/sec on the Cornell box (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): objs/cornellroom.sdl, 512x512 pixels,
+64 spp, 4 bounces per GPU.  One step = one render of that image (the whole
+main.py:186-280 loop) with the scene already resident in HBM; the framebuffer
+stays in HBM.  With N GPUs (one process per GPU, torch.distributed over RCCL)
+the job is a 512 x (512*N) image: rank r renders the rows iy % N == r (512 rows,
+a fixed per-GPU share -> weak scaling) and one RCCL gather collects the row
+tiles on rank 0 inside the timed step.
+
+Printed on rank 0: one JSON line with the driver's fields plus
+  roofline     : dominant kernel (k_render) achieved FP32 rate from the
+                 reference-semantics ray-triangle test count (exact, from a
+                 counting launch) x 47 FLOP/test over the
+                 HIP-event kernel time, against the 157.3 TF FP32 peak; traffic
+                 from the committed rocprofv3 PMC pass (profiles/)
+  cpu_baseline : the C oracle (a restatement of the reference loop, test
+                 infrastructure) timed on this host on a row sample
+  linf_vs_cpu_ref : per-pixel L-inf of this run's framebuffer vs the oracle
+                 on sample rows
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+W = 512
+H_PER_GPU = 512
+SPP = 64
+BOUNCES = 4
+SEED = 9
+FLOP_PER_TEST = 47          # Moller-Trumbore with line semantics
+FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-check", action="store_true", help="skip L-inf vs the CPU oracle")
+    return ap.parse_args()
+
+
+def load_traffic():
+    p = os.path.join(ROOT, "profiles", "traffic_k2.json")
+    if not os.path.exists(p):
+        return None, None
+    with open(p) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), d.get("source")
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from pathtracerpython_amd import scene_reader
+    from pathtracerpython_amd.distributed import assemble, gather_tiles
+    from pathtracerpython_amd.render import Renderer
+    scene_reader.VERBOSE = False
+    scene = scene_reader.Scene(os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl"))
+    H = H_PER_GPU * world
+    r = Renderer(scene)
+    p = r.params(W, H, SPP, BOUNCES, SEED, row_begin=0, row_end=H, row_step=world,
+                 row_phase=rank)
+    rows = r.band_rows(p)
+    assert rows == H_PER_GPU
+    stream = torch.cuda.current_stream()
+    tile = torch.zeros((rows, W, 3), dtype=torch.float32, device="cuda")
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        r.render_device(p, tile.data_ptr(), stream.cuda_stream)
+        if ev:
+            ev[1].record(stream)
+        if world > 1:
+            return gather_tiles(tile)
+        return [tile]
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # HIP events around every render launch, on the stream it is launched on
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out = step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    ms_per_step = elapsed / args.steps * 1e3
+    paths = W * H * SPP
+    value = paths / (elapsed / args.steps) / 1e6
+
+    result = None
+    if rank == 0:
+        # exact reference-semantics work of one launch (separate counting launch)
+        pc = r.params(W, H, SPP, BOUNCES, SEED, count=True, row_begin=0, row_end=H,
+                      row_step=world, row_phase=rank)
+        _, st = r.render_params(pc, stats=True)
+        tests = st["closest_tests"] + st["shadow_tests"]
+        k_ms = float(np.mean(kernel_ms))
+        achieved = tests * FLOP_PER_TEST / (k_ms * 1e-3) / 1e12
+        traffic, tsrc = load_traffic()
+        roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                    "traffic": traffic,
+                    "kernel": "k_render<false,false>",
+                    "compute_pipe": "VALU f32 (no MFMA: scalar intersection; the MI355X f32 "
+                                    "vector peak equals the f32 MFMA dense peak)",
+                    "work_per_launch": {"ray_triangle_tests": tests,
+                                        "tests_per_path_sample": round(tests / (W * H_PER_GPU * SPP), 2),
+                                        "flop_per_test": FLOP_PER_TEST,
+                                        "f64_fallback_tests": st["f64_fallbacks"],
+                                        "f64_rescans": st["f64_rescans"]},
+                    "kernel_ms_mean": round(k_ms, 4),
+                    "hbm_frac": (round(traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
+                                 if traffic else None),
+                    "traffic_source": tsrc}
+        # correctness of this run: per-pixel L-inf vs the CPU oracle on sample rows
+        linf = None
+        fb = None
+        if not args.no_check or not args.no_cpu_baseline:
+            from oracle import oracle
+            tiles = [t.cpu().numpy() for t in out]
+            fb = assemble(tiles, H) if world > 1 else tiles[0]
+        if not args.no_check:
+            from oracle import oracle
+            chk_rows = [0, 129, 255, H - 1]
+            pix = np.array([ix * H + iy for iy in chk_rows for ix in range(W)], dtype=np.int64)
+            ref, _ = oracle.render(r.packed, W, H, SPP, BOUNCES, SEED, pixels=pix,
+                                   threads=args.cpu_threads)
+            got = np.stack([fb[H - 1 - iy] for iy in chk_rows]).reshape(-1, 3).astype(np.float64)
+            linf = float(np.abs(got - ref).max())
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            from oracle import oracle
+            sample_rows = list(range(0, H))
+            pix = np.array([ix * H + iy for iy in sample_rows for ix in range(W)], dtype=np.int64)
+            threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+            t1 = time.perf_counter()
+            oracle.render(r.packed, W, H, SPP, BOUNCES, SEED, pixels=pix, threads=threads)
+            cdt = time.perf_counter() - t1
+            cpu = {"value": round(len(pix) * SPP / cdt / 1e6, 4), "unit": "Mpath-samples/s",
+                   "cores": threads, "kind": "port",
+                   "sample": f"oracle/pt_oracle.c (f64 C restatement of main.py:186-280) on "
+                             f"the whole 512x512 64spp 4-bounce job "
+                             f"({len(pix) * SPP} path samples, {cdt:.1f} s, {threads} threads)"}
+        result = {
+            "metric": "Mega path-samples/sec on Cornell box; per-pixel L-inf vs CPU ref",
+            "value": round(value, 2), "unit": "Mpath-samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32+f64", "data": "synthetic",
+            "config": {"workload": "Cornell box (objs/cornellroom.sdl) 512x512 64 spp 4 bounces "
+                                   "per GPU; N GPUs render 512x(512N) rows-interleaved + RCCL gather",
+                       "width": W, "height": H, "spp": SPP, "bounces": BOUNCES, "seed": SEED,
+                       "parallelism": f"rows/{world}" + (" + rccl gather" if world > 1 else "")},
+            "linf_vs_cpu_ref": linf,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    r.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

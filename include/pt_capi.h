@@ -42,6 +42,8 @@ extern "C" {
 #define PT_FLAG_FORCE_F64 (1u << 1)    /* send every intersection test to the
                                           f64 evaluator (self-check mode) */
 #define PT_FLAG_COUNT (1u << 2)        /* fill pt_stats counters (slower) */
+#define PT_FLAG_OUT_F64 (1u << 3)      /* framebuffer elements are float64
+                                          (default float32)              */
 
 /*
  * Flattened scene, as produced by scene_reader.Scene
@@ -69,8 +71,8 @@ typedef struct pt_scene_desc {
  * (utils.py:64-69).  Rows: a launch renders the image rows iy with
  * row_begin <= iy < row_end and iy % row_step == row_phase, which covers
  * contiguous bands (row_step 1) and the interleaved bands used for
- * multi-GPU balance.  Output: image orientation, float32
- * out[(height-1-iy)][ix][3] restricted to the launched rows, packed in
+ * multi-GPU balance.  Output: image orientation, float32 (float64 with
+ * PT_FLAG_OUT_F64) out[(height-1-iy)][ix][3] restricted to the launched rows, packed in
  * launch order (see pt_band_rows).  Values are the averaged radiance before
  * make_image's min-max normalisation (main.py:274-280).                    */
 typedef struct pt_render_params {
@@ -116,14 +118,15 @@ void pt_scene_destroy(pt_scene* scene);
 int pt_band_rows(const pt_render_params* p, int32_t* rows);
 
 /* Whole loop main.py:186-280 for the selected rows.  out_rgb_dev is a DEVICE
- * pointer (float32, rows*width*3), written on `stream` (a hipStream_t, or
- * NULL for the null stream).  Asynchronous; pt_last_kernel_ms() reads the
- * HIP-event time of the most recent launch after the stream has synced. */
+ * pointer (rows*width*3 float32, or float64 with PT_FLAG_OUT_F64), written on
+ * `stream` (a hipStream_t, or NULL for the null stream).  Asynchronous unless
+ * stats are requested with PT_FLAG_COUNT; pt_last_kernel_ms() reads the
+ * HIP-event time of the most recent launch. */
 int pt_render_device(pt_scene* scene, const pt_render_params* p,
-                     float* out_rgb_dev, void* stream, pt_stats* stats);
+                     void* out_rgb_dev, void* stream, pt_stats* stats);
 
-/* Same, synchronous, with a host output buffer (rows*width*3 float32). */
-int pt_render(pt_scene* scene, const pt_render_params* p, float* out_rgb_host,
+/* Same, synchronous, with a host output buffer (rows*width*3 elements). */
+int pt_render(pt_scene* scene, const pt_render_params* p, void* out_rgb_host,
               pt_stats* stats);
 
 /* Kernel time (ms) of the last pt_render_device launch on this handle. */

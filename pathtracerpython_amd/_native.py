@@ -31,7 +31,7 @@ def _bind(lib):
         "pt_scene_destroy": ([vp], None),
         "pt_band_rows": ([C.POINTER(PtRenderParams), ip], C.c_int),
         "pt_render_device": ([vp, C.POINTER(PtRenderParams), vp, vp, C.POINTER(PtStats)], C.c_int),
-        "pt_render": ([vp, C.POINTER(PtRenderParams), C.POINTER(C.c_float), C.POINTER(PtStats)], C.c_int),
+        "pt_render": ([vp, C.POINTER(PtRenderParams), vp, C.POINTER(PtStats)], C.c_int),
         "pt_last_kernel_ms": ([vp, C.POINTER(C.c_float)], C.c_int),
         "pt_intersect_objects": ([vp, dp, C.c_int64, ip, dp], C.c_int),
         "pt_compute_color": ([vp, ip, dp, dp, dp, C.c_int64, dp], C.c_int),

@@ -42,6 +42,7 @@ struct RenderK {
     int32_t sample_begin;
     uint32_t split, split_log2;
     uint32_t npix;
+    int32_t out_f64;
 };
 
 struct StatsDev { unsigned long long v[8]; };
@@ -61,7 +62,7 @@ __device__ __forceinline__ void flush_counters(const Counters& c, StatsDev* st) 
 }
 
 template <bool FORCE64, bool COUNT>
-__global__ __launch_bounds__(256) void k_render(SceneK S, RenderK R, float* __restrict__ out,
+__global__ __launch_bounds__(256) void k_render(SceneK S, RenderK R, void* __restrict__ out,
                                                 StatsDev* __restrict__ st) {
     const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t pl = tid >> R.split_log2;
@@ -98,12 +99,16 @@ __global__ __launch_bounds__(256) void k_render(SceneK S, RenderK R, float* __re
         acc.y += __shfl_xor(acc.y, (int)m);
         acc.z += __shfl_xor(acc.z, (int)m);
     }
-    if (valid && c == 0) {
+    if (valid && c == 0) {   // pixel_color_list[i] / how_many_rays, main.py:277
         const double inv = (double)R.spp;
-        float* o = out + ((size_t)(R.n_rows - 1 - row_local) * (size_t)R.W + (size_t)ix) * 3;
-        o[0] = (float)(acc.x / inv);
-        o[1] = (float)(acc.y / inv);
-        o[2] = (float)(acc.z / inv);
+        const size_t e = ((size_t)(R.n_rows - 1 - row_local) * (size_t)R.W + (size_t)ix) * 3;
+        if (R.out_f64) {
+            double* o = (double*)out + e;
+            o[0] = acc.x / inv; o[1] = acc.y / inv; o[2] = acc.z / inv;
+        } else {
+            float* o = (float*)out + e;
+            o[0] = (float)(acc.x / inv); o[1] = (float)(acc.y / inv); o[2] = (float)(acc.z / inv);
+        }
     }
     flush_counters<COUNT>(cnt, st);
 }
@@ -149,7 +154,7 @@ struct pt_scene {
     float xbound = 0.f;
     void* blob = nullptr;          // all scene tables, one allocation
     StatsDev* stats = nullptr;
-    float* out_dev = nullptr;      // pt_render's staging buffer
+    void* out_dev = nullptr;       // pt_render's staging buffer
     size_t out_cap = 0;
     hipStream_t stream = nullptr;  // pt_render's own stream
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -309,7 +314,7 @@ static uint32_t choose_split(uint32_t npix, int32_t spp) {
     return s;
 }
 
-int pt_render_device(pt_scene* s, const pt_render_params* p, float* out_dev, void* stream,
+int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void* stream,
                      pt_stats* stats) {
     if (!s) return fail(PT_EINVAL, "null scene");
     int rc = validate(p);
@@ -326,6 +331,7 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, float* out_dev, voi
     R.rr_depth = (p->flags & PT_FLAG_RR) ? std::max(0, p->rr_depth) : -1;
     R.first_row = first; R.row_step = p->row_step; R.n_rows = rows;
     R.sample_begin = p->sample_begin;
+    R.out_f64 = (p->flags & PT_FLAG_OUT_F64) ? 1 : 0;
     R.npix = (uint32_t)rows * (uint32_t)p->width;
     R.split = choose_split(R.npix, p->spp);
     R.split_log2 = 0;
@@ -365,7 +371,7 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, float* out_dev, voi
     return PT_OK;
 }
 
-int pt_render(pt_scene* s, const pt_render_params* p, float* out_host, pt_stats* stats) {
+int pt_render(pt_scene* s, const pt_render_params* p, void* out_host, pt_stats* stats) {
     if (!s) return fail(PT_EINVAL, "null scene");
     int rc = validate(p);
     if (rc) return rc;
@@ -374,12 +380,13 @@ int pt_render(pt_scene* s, const pt_render_params* p, float* out_host, pt_stats*
     if (rows == 0) return PT_OK;
     if (!out_host) return fail(PT_EINVAL, "null output");
     DeviceGuard g(s->device);
-    const size_t bytes = (size_t)rows * p->width * 3 * sizeof(float);
+    const size_t elem = (p->flags & PT_FLAG_OUT_F64) ? sizeof(double) : sizeof(float);
+    const size_t bytes = (size_t)rows * p->width * 3 * elem;
     if (bytes > s->out_cap) {
         if (s->out_dev) (void)hipFree(s->out_dev);
         s->out_dev = nullptr;
         s->out_cap = 0;
-        HIPCHK(hipMalloc((void**)&s->out_dev, bytes));
+        HIPCHK(hipMalloc(&s->out_dev, bytes));
         s->out_cap = bytes;
     }
     rc = pt_render_device(s, p, s->out_dev, s->stream, stats);

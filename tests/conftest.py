@@ -1,0 +1,98 @@
+"""Shared fixtures.  `gpu`-marked tests need an MI355X (run on the GPU box with
+`pytest -m gpu`); everything else runs on CPU in the build container."""
+import ctypes as C
+import glob
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+CORNELL = os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl")
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and libpt_hip.so")
+
+
+@pytest.fixture(scope="session")
+def cornell():
+    from pathtracerpython_amd import scene_reader
+    scene_reader.VERBOSE = False
+    return scene_reader.Scene(CORNELL)
+
+
+@pytest.fixture(scope="session")
+def packed(cornell):
+    from pathtracerpython_amd.pack import pack_scene
+    return pack_scene(cornell)
+
+
+def golden_renders():
+    out = []
+    for f in sorted(glob.glob(os.path.join(GOLDEN, "render_*.npz"))):
+        g = np.load(f)
+        out.append((os.path.basename(f), {k: g[k] for k in g.files}))
+    return out
+
+
+@pytest.fixture(scope="session")
+def kat():
+    g = np.load(os.path.join(GOLDEN, "kat_cornell.npz"))
+    return {k: g[k] for k in g.files}
+
+
+@pytest.fixture(scope="session")
+def hostcheck():
+    """Host build of the kernel's per-lane code (tests/hostcheck)."""
+    d = os.path.join(ROOT, "tests", "hostcheck")
+    subprocess.run(["make", "-s", "-C", d], check=True)
+    lib = C.CDLL(os.path.join(d, "build", "libhostcheck.so"))
+    lib.hc_render.restype = C.c_int
+    lib.hc_filter_selftest.restype = C.c_int
+    return lib
+
+
+def hc_render(lib, packed, params, force64=False):
+    from pathtracerpython_amd._abi import band_rows
+    rows = len(band_rows(params.height, params.row_begin, params.row_end, params.row_step,
+                         params.row_phase))
+    out = np.zeros((rows, params.width, 3), dtype=np.float64)
+    cnt = (C.c_uint64 * 8)()
+    rc = lib.hc_render(C.byref(packed.desc), C.byref(params), int(force64),
+                       out.ctypes.data_as(C.POINTER(C.c_double)), cnt)
+    assert rc == 0
+    names = ("closest_tests", "shadow_tests", "ray_bounces", "shading_points", "light_hits",
+             "escapes", "f64_fallbacks", "f64_rescans")
+    return out, dict(zip(names, (int(x) for x in cnt)))
+
+
+def random_scene(tmp_path, n_tris, seed, light_scale=1.0):
+    """A Cornell variant with an extra random-triangle object (plain v/f OBJ,
+    same ingest as the reference's), written to tmp_path."""
+    import shutil
+    rs = np.random.RandomState(seed)
+    src = os.path.dirname(CORNELL)
+    for f in os.listdir(src):
+        shutil.copy(os.path.join(src, f), tmp_path / f)
+    c = rs.uniform([-3.5, -3.5, -32.0], [3.5, 3.5, -17.0], (n_tris, 3))
+    lines = []
+    for i in range(n_tris):
+        for _ in range(3):
+            v = c[i] + rs.normal(0, 0.6, 3)
+            lines.append("v %.9f %.9f %.9f" % tuple(v))
+    for i in range(n_tris):
+        lines.append("f %d %d %d" % (3 * i + 1, 3 * i + 2, 3 * i + 3))
+    (tmp_path / "rand.obj").write_text("\n".join(lines) + "\n")
+    sdl = open(CORNELL).read().replace(
+        "output cornell.pnm",
+        "object rand.obj 0.2 0.5 0.9 0.3 0.6 0.4 0 3\noutput cornell.pnm")
+    (tmp_path / "scene.sdl").write_text(sdl)
+    from pathtracerpython_amd import scene_reader
+    scene_reader.VERBOSE = False
+    return scene_reader.Scene(str(tmp_path / "scene.sdl"))

@@ -1,0 +1,104 @@
+"""C-ABI of libpt_hip.so: loads without a GPU, exports every entry point
+include/pt_capi.h declares, validates arguments, and fails loudly (no CPU
+fallback) when no gfx950 device is present."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from pathtracerpython_amd import _native
+from pathtracerpython_amd._abi import PtRenderParams, PtSceneDesc, PtStats, band_rows, make_params
+
+HEADER = os.path.join(ROOT, "include", "pt_capi.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pt_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_expected_api():
+    assert set(declared_functions()) == set(_native.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    lib = _native.lib()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+
+
+def test_abi_struct_layout():
+    # offsets the C side relies on (include/pt_capi.h)
+    assert C.sizeof(PtSceneDesc) == 4 * 4 + 5 * 8 + 8 * (3 + 4 + 1 + 3)
+    assert C.sizeof(PtRenderParams) == 4 * 4 + 8 + 4 * 8
+    assert C.sizeof(PtStats) == 8 * 8
+
+
+def test_api_version():
+    assert _native.lib().pt_api_version() == 1
+
+
+@pytest.mark.parametrize("H,step,phase,b,e", [(10, 1, 0, 0, 10), (10, 3, 1, 0, 10),
+                                              (10, 4, 3, 0, 10), (7, 2, 0, 3, 6),
+                                              (5, 8, 6, 0, 5), (9, 1, 0, 9, 9)])
+def test_band_rows_matches_python(H, step, phase, b, e):
+    p = make_params(4, H, 1, 1, 0, row_begin=b, row_end=e, row_step=step, row_phase=phase)
+    n = C.c_int32(-1)
+    assert _native.lib().pt_band_rows(C.byref(p), C.byref(n)) == 0
+    assert n.value == len(band_rows(H, b, e, step, phase))
+
+
+def test_band_rows_rejects_bad_step():
+    p = make_params(4, 4, 1, 1, 0, row_step=2, row_phase=2)
+    n = C.c_int32()
+    assert _native.lib().pt_band_rows(C.byref(p), C.byref(n)) == -1
+    assert "row_step" in _native.last_error()
+
+
+def test_scene_create_validates(packed):
+    lib = _native.lib()
+    h = C.c_void_p()
+    assert lib.pt_scene_create(None, C.byref(h)) != 0
+    bad = PtSceneDesc()
+    C.memmove(C.byref(bad), C.byref(packed.desc), C.sizeof(PtSceneDesc))
+    bad.n_obj_tri = bad.n_tri   # light without triangles
+    rc = lib.pt_scene_create(C.byref(bad), C.byref(h))
+    assert rc in (-1, -4)   # EINVAL, or ENODEV first when no GPU is visible
+
+
+def test_no_gpu_fails_loudly(packed):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from pathtracerpython_amd.render import Renderer
+    with pytest.raises(_native.NativeError, match="no HIP device|gfx950"):
+        Renderer(_load_cornell())
+
+
+def _load_cornell():
+    from pathtracerpython_amd import scene_reader
+    scene_reader.VERBOSE = False
+    return scene_reader.Scene(os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl"))
+
+
+def test_missing_library_is_an_error(monkeypatch, tmp_path):
+    monkeypatch.setattr(_native, "_lib", None)
+    monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(_native.NativeError, match="no CPU fallback"):
+        _native.lib()
+
+
+def test_list_order_roundtrip():
+    from pathtracerpython_amd.render import from_list_order, to_list_order
+    W, H = 5, 3
+    cols = np.arange(W * H * 3, dtype=np.float64).reshape(W * H, 3)
+    fb = from_list_order(cols, W, H)
+    # k = ix*H + iy sits at fb[H-1-iy, ix]
+    for k in range(W * H):
+        ix, iy = divmod(k, H)
+        assert np.array_equal(fb[H - 1 - iy, ix], cols[k])
+    assert np.array_equal(to_list_order(fb), cols)

@@ -1,0 +1,99 @@
+"""The render kernel's per-lane code (pt_path.h / pt_core.h), compiled for the
+host (tests/hostcheck), against the oracle and the reference goldens.  This
+is where the f32 filter's correctness is checked on CPU: its certain verdicts
+must never disagree with the f64 evaluation, and a hybrid render must equal
+the forced-f64 render bit for bit."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import golden_renders, hc_render, random_scene
+from oracle import oracle
+from pathtracerpython_amd._abi import PT_FLAG_RR, make_params
+from pathtracerpython_amd.pack import pack_scene
+from pathtracerpython_amd.render import to_list_order
+
+
+def selftest(lib, packed, n, seed):
+    out = (C.c_int64 * 4)()
+    assert lib.hc_filter_selftest(C.byref(packed.desc), C.c_int64(n), C.c_uint64(seed), out) == 0
+    return list(out)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_filter_never_wrong_cornell(hostcheck, packed, seed):
+    wrong, amb, tests, cand = selftest(hostcheck, packed, 20000, seed)
+    assert wrong == 0
+    assert cand > 0 and amb < 0.02 * tests
+
+
+@pytest.mark.parametrize("n_tris,seed", [(40, 11), (200, 12)])
+def test_filter_never_wrong_random_mesh(hostcheck, tmp_path, n_tris, seed):
+    pk = pack_scene(random_scene(tmp_path, n_tris, seed))
+    wrong, amb, tests, cand = selftest(hostcheck, pk, 3000, seed)
+    assert wrong == 0 and cand > 0
+
+
+@pytest.mark.parametrize("name,g", golden_renders(), ids=[n for n, _ in golden_renders()])
+@pytest.mark.parametrize("force64", [False, True])
+def test_kernel_code_matches_reference(hostcheck, packed, name, g, force64):
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    fb, st = hc_render(hostcheck, packed, make_params(W, H, spp, B, seed), force64)
+    assert np.abs(to_list_order(fb) - g["colors"]).max() <= 1e-12
+    _, ost = oracle.render(packed, W, H, spp, B, seed)
+    for k in ("closest_tests", "shadow_tests", "ray_bounces", "shading_points", "light_hits",
+              "escapes"):
+        assert st[k] == ost[k], k
+
+
+@pytest.mark.parametrize("W,H,spp,B,flags", [(40, 40, 3, 6, 0), (33, 17, 2, 8, PT_FLAG_RR),
+                                             (1, 1, 5, 4, 0), (8, 8, 2, 0, 0)])
+def test_hybrid_bitwise_equals_f64(hostcheck, packed, W, H, spp, B, flags):
+    p = make_params(W, H, spp, B, 77, flags)
+    a, sa = hc_render(hostcheck, packed, p, False)
+    b, sb = hc_render(hostcheck, packed, p, True)
+    assert np.array_equal(a, b)
+    ref, _ = oracle.render(packed, W, H, spp, B, 77, flags)
+    assert np.abs(to_list_order(a) - ref).max() <= 1e-12
+    if B == 0:
+        assert not a.any()
+
+
+def test_random_mesh_scene(hostcheck, tmp_path):
+    pk = pack_scene(random_scene(tmp_path, 60, 5))
+    p = make_params(24, 24, 2, 4, 3)
+    a, _ = hc_render(hostcheck, pk, p, False)
+    b, _ = hc_render(hostcheck, pk, p, True)
+    assert np.array_equal(a, b)
+    ref, _ = oracle.render(pk, 24, 24, 2, 4, 3)
+    assert np.abs(to_list_order(a) - ref).max() <= 1e-12
+
+
+def test_interleaved_bands_concat_to_full(hostcheck, packed):
+    from pathtracerpython_amd.distributed import assemble, max_band_rows
+    W = H = 20
+    full, _ = hc_render(hostcheck, packed, make_params(W, H, 2, 3, 4))
+    world = 3
+    tiles = []
+    for r in range(world):
+        t, _ = hc_render(hostcheck, packed, make_params(W, H, 2, 3, 4, row_step=world, row_phase=r))
+        pad = np.zeros((max_band_rows(H, world), W, 3))
+        pad[:t.shape[0]] = t
+        tiles.append(pad)
+    assert np.array_equal(assemble(tiles, H), full)
+
+
+def test_contiguous_band(hostcheck, packed):
+    W = H = 16
+    full, _ = hc_render(hostcheck, packed, make_params(W, H, 1, 3, 4))
+    band, _ = hc_render(hostcheck, packed, make_params(W, H, 1, 3, 4, row_begin=5, row_end=11))
+    assert np.array_equal(band, full[H - 11:H - 5])
+
+
+def test_sample_split_is_linear(hostcheck, packed):
+    W = H = 12
+    full, _ = hc_render(hostcheck, packed, make_params(W, H, 4, 3, 8))
+    a, _ = hc_render(hostcheck, packed, make_params(W, H, 2, 3, 8, sample_begin=0))
+    b, _ = hc_render(hostcheck, packed, make_params(W, H, 2, 3, 8, sample_begin=2))
+    assert np.abs((a + b) / 2 - full).max() <= 1e-14
