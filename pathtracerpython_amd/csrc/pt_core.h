@@ -23,6 +23,8 @@
 
 #define PT_HD __host__ __device__ __forceinline__
 
+#include "pt_math.h"
+
 namespace pt {
 
 constexpr double kZero = 1e-5;        // main.py:20, utils.py:18
@@ -142,9 +144,8 @@ PT_HD double squared_dist(D3 a, D3 b) {
     const double dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
     return ((0.0 + dx * dx) + dy * dy) + dz * dz;
 }
-PT_HD D3 unit(D3 a) {   // v / np.linalg.norm(v), with one reciprocal
-    const double inv = 1.0 / sqrt(dot(a, a));
-    return a * inv;
+PT_HD D3 unit(D3 a) {   // v / np.linalg.norm(v), as v * rsqrt(v.v)
+    return a * rsqrt_d(dot(a, a));
 }
 PT_HD F3 to_f3(D3 a) { F3 r; r.x = (float)a.x; r.y = (float)a.y; r.z = (float)a.z; return r; }
 
@@ -158,7 +159,7 @@ PT_HD bool eval64(const TriD& T, D3 o, D3 dn, D3* P, double* sqd) {
     const D3 vp = ld3(T.vp);
     const double den = dot(dn, vp);
     if (!(fabs(den) > kZero)) return false;
-    const double t = (T.cvp - dot(vp, o)) / dot(vp, dn);
+    const double t = (T.cvp - dot(vp, o)) * rcp_d(dot(vp, dn));
     const D3 p = o + dn * t;
     const D3 c1 = cross(ld3(T.e12), p - ld3(T.v2));
     const D3 c2 = cross(ld3(T.e23), p - ld3(T.v3));
@@ -198,18 +199,19 @@ PT_HD OriginF origin_f(const TriF& T, F3 o) {
     return r;
 }
 
-// Core classification.  Returns kMiss when the reference certainly reports
-// "no intersection usable in range", kCand when it certainly reports an
-// intersection inside the triangle with |t| in (lo, hi) (|t| interval
-// [t-dt, t+dt] returned), kAmb otherwise.  Range semantics:
-//   closest: valid iff sqd > 1e-5                 -> lo = kTz, hi = inf
-//   shadow : occluder iff 1e-5 <= sqd < |L - P|^2 -> lo = kTz, hi = tL
+// Core classification (branch-free: on a 64-lane wave the lanes rarely agree
+// on an early exit, so everything is computed and selected).  Returns kMiss
+// when the reference certainly reports "no intersection usable in range",
+// kCand when it certainly reports an intersection inside the triangle with
+// |t| in range (|t| interval [t-dt, t+dt] returned), kAmb otherwise.
+// Range semantics:
+//   closest: valid iff sqd > 1e-5                 -> hi = inf
+//   shadow : occluder iff 1e-5 <= sqd < |L - P|^2 -> hi = tL (hi_lo/hi_hi
+//            bracket tL with slack)
 PT_HD int classify(const TriF& T, const OriginF& O, F3 d, float hi_lo, float hi_hi,
                    float* t_abs, float* t_err) {
     const float q = lin3(T.n, d);
     const float aq = fabsf(q);
-    if (aq < T.qlo) return kMiss;                       // certainly |dot| <= 1e-5
-    const bool par_amb = !(aq > T.qhi);
     const float r = rcpf(q);
     const float t = -O.h * r;
     const float at = fabsf(t);
@@ -220,16 +222,16 @@ PT_HD int classify(const TriF& T, const OriginF& O, F3 d, float hi_lo, float hi_
     // |beta_ref - beta| <= del2, |gamma_ref - gamma| <= del2,
     // |alpha_ref - alpha| <= 2*del2 (alpha = 1 - beta - gamma, two roundings)
     const float del2 = fmaf(T.g, dt, fmaf(at, T.ed, T.eo)) + 8.0f * kU;
-    // certainly outside: some weight certainly negative (miss whether or not
-    // the reference's parallel test fires)
-    if (min3f(beta, gam, alpha + del2) < -del2) return kMiss;
-    if (at + dt < kTzLo) return kMiss;                  // certainly |P - o|^2 < 1e-5
-    if (at - dt >= hi_hi) return kMiss;                 // certainly beyond the range
+    // certainly a miss: |dot| certainly <= 1e-5 (parallel reject), or a
+    // weight certainly negative, or |P - o|^2 certainly < 1e-5, or certainly
+    // beyond the range
+    const bool miss = (aq < T.qlo) | (min3f(beta, gam, alpha + del2) < -del2) |
+                      (at + dt < kTzLo) | (at - dt >= hi_hi);
+    const bool cand = (aq > T.qhi) & (min3f(beta, gam, alpha - del2) > del2) &
+                      (at - dt > kTzHi) & (at + dt < hi_lo);
     *t_abs = at;
     *t_err = dt;
-    const bool inside = min3f(beta, gam, alpha - del2) > del2;
-    const bool in_range = (at - dt > kTzHi) && (at + dt < hi_lo);
-    return (!par_amb && inside && in_range) ? kCand : kAmb;
+    return miss ? kMiss : (cand ? kCand : kAmb);
 }
 
 // ------------------------------------------------------ light sampling --
@@ -243,7 +245,7 @@ PT_HD int pick_light(const SceneK& S, double u) {
 
 // sample_random_pt with sample_bary_coords, utils.py:21-25, :42-46
 PT_HD D3 light_point(const TriD& T, double u1, double u2, double u3) {
-    const double inv = 1.0 / (((0.0 + u1) + u2) + u3);
+    const double inv = rcp_d(((0.0 + u1) + u2) + u3);
     const double a = u1 * inv, b = u2 * inv, c = u3 * inv;
     return d3(a * T.v1[0] + b * T.v2[0] + c * T.v3[0],
               a * T.v1[1] + b * T.v2[1] + c * T.v3[1],
@@ -255,13 +257,21 @@ PT_HD D3 rotate_y(const TriS& R, D3 v) {   // np.dot(rotation_matrix, v)
     return d3(R.r00 * v.x + R.r02 * v.z, R.r11 * v.y, R.r20 * v.x + R.r22 * v.z);
 }
 
+// x ** n for a non-integer exponent: the general f64 pow, kept out of line —
+// inlined it costs the kernel ~40 VGPRs for a path the Cornell materials
+// (n = 5) never take.  `const`: no memory effects, so the call does not stop
+// the compiler from using scalar loads for the uniform scene reads.
+__host__ __device__ __attribute__((noinline, const)) inline double pow_general(double x, double n) {
+    return pow(x, n);
+}
+
 PT_HD double pow_ref(double x, const Mat& m) {   // x ** n (numpy float power)
-    if (m.nint >= 0 && m.nint <= 16) {
+    if (m.nint >= 0) {
         double r = 1.0;
+#pragma unroll 1
         for (int i = 0; i < m.nint; ++i) r *= x;
         return r;
     }
-    return pow(x, m.nexp);
+    return pow_general(x, m.nexp);
 }
-
 }  // namespace pt

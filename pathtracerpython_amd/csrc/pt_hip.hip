@@ -62,8 +62,13 @@ __device__ __forceinline__ void flush_counters(const Counters& c, StatsDev* st) 
 }
 
 template <bool FORCE64, bool COUNT>
-__global__ __launch_bounds__(256) void k_render(SceneK S, RenderK R, void* __restrict__ out,
+// 4 waves/SIMD (<= 128 VGPRs, a little scratch spill outside the triangle
+// loops): 9.5 ms vs 10.8 ms at 3 waves and 15.3 ms at 2 on the 512^2 x 64spp
+// bench (MI355X), see DESIGN.md §5.
+__global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __restrict__ out,
                                                 StatsDev* __restrict__ st) {
+    __shared__ double spill[kSpillSlots][256];
+    const Spill sp{&spill[0][threadIdx.x], 256};
     const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t pl = tid >> R.split_log2;
     const uint32_t c = tid & (R.split - 1u);
@@ -91,8 +96,8 @@ __global__ __launch_bounds__(256) void k_render(SceneK S, RenderK R, void* __res
         J.rr_depth = R.rr_depth;
         D3 P0 = d3(0, 0, 0);
         int tri0 = -1;
-        if (ns > 0 && R.bounces > 0) tri0 = closest<FORCE64, false>(S, eye, d0, -1, &P0, &cnt);
-        acc = render_lane<FORCE64, COUNT>(S, J, eye, d0, tri0, P0, &cnt);
+        if (ns > 0 && R.bounces > 0) tri0 = closest<FORCE64, false>(S, eye, d0, -1, sp, &P0, &cnt);
+        acc = render_lane<FORCE64, COUNT>(S, J, d0, tri0, P0, sp, &cnt);
     }
     for (uint32_t m = 1; m < R.split; m <<= 1) {
         acc.x += __shfl_xor(acc.x, (int)m);
@@ -116,6 +121,8 @@ __global__ __launch_bounds__(256) void k_render(SceneK S, RenderK R, void* __res
 __global__ __launch_bounds__(256) void k_intersect(SceneK S, const double* __restrict__ rays,
                                                    int64_t n, float xb, int32_t* __restrict__ out_tri,
                                                    double* __restrict__ out_p) {
+    __shared__ double spill[kSpillSlots][256];
+    const Spill sp{&spill[0][threadIdx.x], 256};
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const D3 o = ld3(rays + 6 * i), d = ld3(rays + 6 * i + 3);
@@ -123,7 +130,7 @@ __global__ __launch_bounds__(256) void k_intersect(SceneK S, const double* __res
     const bool in_box = fabsf(oc.x) <= xb && fabsf(oc.y) <= xb && fabsf(oc.z) <= xb;
     D3 P = d3(0, 0, 0);
     Counters c;
-    const int t = in_box ? closest<false, false>(S, o, d, -1, &P, &c) : closest<true, false>(S, o, d, -1, &P, &c);
+    const int t = in_box ? closest<false, false>(S, o, d, -1, sp, &P, &c) : closest<true, false>(S, o, d, -1, sp, &P, &c);
     out_tri[i] = t;
     out_p[3 * i] = P.x; out_p[3 * i + 1] = P.y; out_p[3 * i + 2] = P.z;
 }
@@ -133,6 +140,8 @@ __global__ __launch_bounds__(256) void k_color(SceneK S, const int32_t* __restri
                                                const double* __restrict__ normal,
                                                const double* __restrict__ u, int64_t n, float xb,
                                                double* __restrict__ out) {
+    __shared__ double spill[kSpillSlots][256];
+    const Spill sp{&spill[0][threadIdx.x], 256};
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const D3 P = ld3(point + 3 * i);
@@ -141,8 +150,8 @@ __global__ __launch_bounds__(256) void k_color(SceneK S, const int32_t* __restri
     const F3 oc = to_f3(P - ld3(S.center));
     const bool in_box = fabsf(oc.x) <= xb && fabsf(oc.y) <= xb && fabsf(oc.z) <= xb;
     Counters c;
-    const D3 col = in_box ? nee<false, false>(S, P, ld3(normal + 3 * i), obj[i], -1, uu, &c)
-                          : nee<true, false>(S, P, ld3(normal + 3 * i), obj[i], -1, uu, &c);
+    const D3 col = in_box ? nee<false, false>(S, P, ld3(normal + 3 * i), obj[i], -1, uu, sp, &c)
+                          : nee<true, false>(S, P, ld3(normal + 3 * i), obj[i], -1, uu, sp, &c);
     out[3 * i] = col.x; out[3 * i + 1] = col.y; out[3 * i + 2] = col.z;
 }
 
@@ -309,7 +318,7 @@ static uint32_t choose_split(uint32_t npix, int32_t spp) {
         return s;
     }
     uint32_t s = 1;
-    const uint64_t target = (uint64_t)1 << 20;   // ~16k waves: 2 rounds of 8 waves x 256 CUs x 4
+    const uint64_t target = (uint64_t)1 << 21;   // ~32k waves: ~8 rounds of 4 waves x 4 SIMDs x 256 CUs
     while (s < cap && (uint64_t)npix * s * 2 <= target) s *= 2;
     return s;
 }

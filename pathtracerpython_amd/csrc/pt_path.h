@@ -4,15 +4,22 @@
 //
 // Reference loop flattened (main.py:186-271): per (pixel, sample) the
 // spp x bounce iteration of the reference becomes an iterative bounce loop in
-// registers; the reference's per-bounce pool phases (main.py:197-231) become
-// closest() and nee() calls.
+// registers.  Per bounce the reference runs two pool phases (closest hit
+// main.py:197-205, colour main.py:208-231) and then samples the next ray
+// (main.py:236-268).  The next ray does not depend on the colour phase, so a
+// bounce here samples it first and runs ONE pass over the triangles that
+// tests the 3 shadow rays (main.py:42-55) and the next ray's closest hit
+// (main.py:94-109) together: the four lines share their origin, so the
+// origin terms of each test are computed once.
 #pragma once
 #include "pt_core.h"
 
 #if defined(__HIP_DEVICE_COMPILE__)
 #define PT_WAVE_ALL(x) (__all(x) != 0)
+#define PT_WAVE_ANY(x) (__any(x) != 0)
 #else
 #define PT_WAVE_ALL(x) (x)
+#define PT_WAVE_ANY(x) (x)
 #endif
 
 namespace pt {
@@ -27,48 +34,72 @@ PT_HD void bump(Counters* c, uint32_t Counters::*f, uint32_t v) {
     if (COUNT) c->*f += v;
 }
 
+// Per-lane f64 scratch that the f32 test loops only touch on a fallback or
+// once per bounce: a home in LDS on the device (structure-of-arrays,
+// conflict-free) that the register allocator can reload from instead of
+// keeping these values live across the loops.  (Not volatile: a volatile
+// access counts as a possible clobber of global memory, which would stop the
+// compiler from using scalar loads for the uniform triangle reads.)  Slots:
+//   0..8  light sample points L_k       9..11  next-ray direction (as the
+//   12..14 ray origin P                        reference holds it, unnormalised)
+//   15..17 primary direction d0
+struct Spill {
+    double* base;
+    int stride;
+    PT_HD double get(int i) const { return base[i * stride]; }
+    PT_HD void put(int i, double v) const { base[i * stride] = v; }
+    PT_HD D3 get3(int i) const { return d3(get(i), get(i + 1), get(i + 2)); }
+    PT_HD void put3(int i, D3 v) const { put(i, v.x); put(i + 1, v.y); put(i + 2, v.z); }
+};
+constexpr int kSpillSlots = 18;
+constexpr int kSpL = 0, kSpNd = 9, kSpP = 12, kSpD0 = 15;
+
 // ----------------------------------------------------------- closest hit --
 // intersect_objects (main.py:83-122): the triangle whose intersection has the
 // smallest squared distance > 1e-5 from the origin, objects first, light
-// last, first minimum wins.  d need not be normalised (utils.py:110).
-// Returns the triangle index (-1 = None) and the hit point P (f64).  ogrp: the
-// coplanar group of the triangle the origin lies on (-1: none / unknown).
-template <bool FORCE64, bool COUNT>
-PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, D3* P, Counters* cnt) {
-    const D3 dn = unit(d);
-    int best = -1;
-    bool decided = false;
-    if (!FORCE64) {
-        const F3 o32 = to_f3(o - ld3(S.center));
-        const F3 d32 = to_f3(dn);
-        float a1 = INFINITY, a2 = INFINITY, b1 = INFINITY;
-        int i1 = -1;
-        for (int t = 0; t < S.n_tri; ++t) {
-            const TriF T = S.trif[t];
-            const OriginF O = origin_f(T, o32);
-            float at = 0.f, dt = 0.f;
-            int st = classify(T, O, d32, INFINITY, INFINITY, &at, &dt);
-            if (T.grp == ogrp) st = kMiss;
-            float a = INFINITY, b = INFINITY;
-            if (st == kCand) { a = at - dt; b = at + dt; }
-            if (st == kAmb) {   // rare: decide this test in f64
-                D3 Q; double sqd;
-                bump<COUNT>(cnt, &Counters::fallbacks, 1);
-                if (eval64(S.trid[t], o, dn, &Q, &sqd) && sqd > kZero) {
-                    const float s = (float)sqrt(sqd);
-                    a = s * (1.0f - 1e-6f);
-                    b = s * (1.0f + 1e-6f);
-                }
-            }
-            if (a < a1) { a2 = a1; a1 = a; b1 = b; i1 = t; }
-            else { a2 = fminf(a2, a); }
+// last, first minimum wins.
+struct ClosestAcc {   // f32 interval bookkeeping of the candidates
+    float a1, a2, b1;
+    int i1;
+};
+PT_HD ClosestAcc closest_init() { ClosestAcc c; c.a1 = c.a2 = c.b1 = INFINITY; c.i1 = -1; return c; }
+PT_HD void closest_add(ClosestAcc* c, int t, float a, float b) {
+    if (a < c->a1) { c->a2 = c->a1; c->a1 = a; c->b1 = b; c->i1 = t; }
+    else { c->a2 = fminf(c->a2, a); }
+}
+
+template <bool COUNT>
+PT_HD void closest_test(const SceneK& S, const TriF& T, const OriginF& O, F3 d32, int t,
+                        bool coplanar, const Spill& sp, int o_slot, int dn_slot,
+                        ClosestAcc* acc, Counters* cnt) {
+    float at = 0.f, dt = 0.f;
+    int st = classify(T, O, d32, INFINITY, INFINITY, &at, &dt);
+    if (coplanar) st = kMiss;
+    float a = (st == kCand) ? at - dt : INFINITY;
+    float b = (st == kCand) ? at + dt : INFINITY;
+    if (st == kAmb) {   // rare: decide this test in f64
+        D3 Q;
+        double sqd;
+        bump<COUNT>(cnt, &Counters::fallbacks, 1);
+        if (eval64(S.trid[t], sp.get3(o_slot), unit(sp.get3(dn_slot)), &Q, &sqd) && sqd > kZero) {
+            const float s = sqrtf((float)sqd);   // |t| to ~1e-7; brackets are 1e-6
+            a = s * (1.0f - 1e-6f);
+            b = s * (1.0f + 1e-6f);
         }
-        // the candidate with the smallest lower bound is certainly the
-        // closest when its interval ends before every other one starts
-        decided = (i1 < 0) || (b1 < a2);
-        best = i1;
     }
-    if (!decided) {   // exact f64 scan (FORCE64, or overlapping intervals)
+    closest_add(acc, t, a, b);
+}
+
+// Finish a closest-hit query: the candidate with the smallest lower bound is
+// certainly the closest when its interval ends before every other one
+// starts; otherwise rescan exactly in f64.  Returns the triangle (-1 = None)
+// and the hit point exactly as the reference computes it.
+template <bool FORCE64, bool COUNT>
+PT_HD int closest_finish(const SceneK& S, const ClosestAcc& c, D3 o, D3 dn, D3* P,
+                         Counters* cnt) {
+    int best = c.i1;
+    const bool decided = !FORCE64 && ((c.i1 < 0) || (c.b1 < c.a2));
+    if (!decided) {
         if (!FORCE64) bump<COUNT>(cnt, &Counters::rescans, 1);
         best = -1;
         double bsq = 0.0;
@@ -80,7 +111,7 @@ PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, D3* P, Counters* cnt) {
             }
         }
     }
-    if (best >= 0) {   // hit point exactly as the reference computes it
+    if (best >= 0) {
         double sqd;
         eval64(S.trid[best], o, dn, P, &sqd);
     }
@@ -89,78 +120,134 @@ PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, D3* P, Counters* cnt) {
     return best;
 }
 
-// ---------------------------------------------------------- direct light --
-// compute_color (main.py:142-145) = compute_ambient_color (main.py:76-80) +
-// compute_shadow_rays (main.py:23-73) at hit point P with normal n on object
-// `obj`.  u: the 12 light-sampling uniforms (slots 0..11).  Occlusion: any
-// OBJECT triangle hit with 1e-5 <= sqd < |P - L|^2 (main.py:42-55, line
-// semantics); the colour factor is that of `obj` after the loop of the LAST
-// shadow ray (main.py:70): its first occluding object, else the last object.
+// Standalone query (primary rays, the batched intersect_objects API).  d need
+// not be normalised (utils.py:110).  ogrp: coplanar group of the triangle the
+// origin lies on (-1: none).
 template <bool FORCE64, bool COUNT>
-PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12], Counters* cnt) {
-    D3 dn[kLightSamples];
-    double lsq[kLightSamples];
-    float hlo[kLightSamples], hhi[kLightSamples];
-    F3 d32[kLightSamples];
-    bool occ[kLightSamples];
-    int first[kLightSamples];
-#pragma unroll
-    for (int k = 0; k < kLightSamples; ++k) {
-        const int li = pick_light(S, u[4 * k]);
-        const D3 L = light_point(S.trid[S.light_tri[li]], u[4 * k + 1], u[4 * k + 2], u[4 * k + 3]);
-        dn[k] = unit(L - P);
-        lsq[k] = squared_dist(P, L);
-        const double tl = sqrt(lsq[k]);
-        hlo[k] = (float)(tl * (1.0 - 1e-6));
-        hhi[k] = (float)(tl * (1.0 + 1e-6));
-        d32[k] = to_f3(dn[k]);
-        occ[k] = false;
-        first[k] = S.n_obj_tri;
-    }
-    int leak = S.n_obj - 1;
-    const F3 o32 = to_f3(P - ld3(S.center));
-    for (int t = 0; t < S.n_obj_tri; ++t) {
-        if (PT_WAVE_ALL(occ[0] && occ[1] && occ[2])) break;
-        const TriF T = S.trif[t];
-        const OriginF O = FORCE64 ? OriginF{0.f, 0.f, 0.f} : origin_f(T, o32);
-        const bool coplanar = (T.grp == ogrp);
-#pragma unroll
-        for (int k = 0; k < kLightSamples; ++k) {
-            if (occ[k]) continue;
-            bool hit;
-            int st = kAmb;
-            if (!FORCE64) {
-                float at, dt;
-                st = classify(T, O, d32[k], hlo[k], hhi[k], &at, &dt);
-                if (coplanar) st = kMiss;
-            }
-            if (st == kAmb) {
-                D3 Q; double sqd;
-                if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
-                hit = eval64(S.trid[t], P, dn[k], &Q, &sqd) && !(sqd < kZero) && sqd < lsq[k];
-            } else {
-                hit = (st == kCand);
-            }
-            if (hit) {
-                occ[k] = true;
-                first[k] = t + 1;
-                if (k == kLightSamples - 1) leak = S.tri_obj[t];
-            }
+PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, const Spill& sp, D3* P, Counters* cnt) {
+    const D3 dn = unit(d);
+    ClosestAcc acc = closest_init();
+    if (!FORCE64) {
+        sp.put3(kSpP, o);
+        sp.put3(kSpNd, d);
+        const F3 o32 = to_f3(o - ld3(S.center));
+        const F3 d32 = to_f3(dn);
+        for (int t = 0; t < S.n_tri; ++t) {
+            const TriF T = S.trif[t];
+            closest_test<COUNT>(S, T, origin_f(T, o32), d32, t, T.grp == ogrp, sp, kSpP, kSpNd,
+                                &acc, cnt);
         }
     }
-    double dsum = 0.0;
+    return closest_finish<FORCE64, COUNT>(S, acc, o, dn, P, cnt);
+}
+
+// ---------------------------------------------------------- direct light --
+// compute_color (main.py:142-145) = compute_ambient_color (main.py:76-80) +
+// compute_shadow_rays (main.py:23-73).  Occlusion: any OBJECT triangle hit
+// with 1e-5 <= sqd < |P - L|^2 (main.py:42-55, line semantics); the colour
+// factor is that of `obj` after the loop of the LAST shadow ray (main.py:70):
+// its first occluding object, else the last object.
+struct ShadowSet {
+    F3 d32[kLightSamples];
+    float hlo[kLightSamples], hhi[kLightSamples];
+    bool occ[kLightSamples];
+    int first[kLightSamples];
+    int leak;
+};
+
+// Light sample k uses the uniforms of slots 4k..4k+3 (one Philox block: the
+// triangle pick utils.py:30 and the three barycentric draws utils.py:23).
+// The points go to the spill; f32 copies of the directions and distance
+// brackets into sh.  `u` is either the 12 explicit uniforms (batched API) or
+// null, in which case block k of (pixel, sample, bounce) is drawn here.
+PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, uint32_t pixel,
+                        uint32_t sample, uint32_t bounce_i, ShadowSet* sh, const Spill& sp) {
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
-        if (!occ[k]) dsum += dot(dn[k], n);
-        bump<COUNT>(cnt, &Counters::shadow_tests, (uint32_t)first[k]);
+        double u0, u1, u2, u3;
+        if (u) {
+            u0 = u[4 * k]; u1 = u[4 * k + 1]; u2 = u[4 * k + 2]; u3 = u[4 * k + 3];
+        } else {
+            uint32_t w[4];
+            rng_block(seed, pixel, sample, bounce_i, (uint32_t)k, w);
+            u0 = u_of(w[0]); u1 = u_of(w[1]); u2 = u_of(w[2]); u3 = u_of(w[3]);
+        }
+        const int li = pick_light(S, u0);
+        const D3 L = light_point(S.trid[S.light_tri[li]], u1, u2, u3);
+        sp.put3(kSpL + 3 * k, L);
+        const D3 dn = unit(L - P);                    // main.py:37-38
+        const float tl = sqrtf((float)squared_dist(P, L));   // main.py:40, to ~2e-7
+        sh->hlo[k] = tl * (1.0f - 1e-6f);
+        sh->hhi[k] = tl * (1.0f + 1e-6f);
+        sh->d32[k] = to_f3(dn);
+        sh->occ[k] = false;
+        sh->first[k] = S.n_obj_tri;
+    }
+    sh->leak = S.n_obj - 1;
+}
+
+template <bool FORCE64, bool COUNT>
+PT_HD void shadow_test(const SceneK& S, const TriF& T, const OriginF& O, int t, bool coplanar,
+                       ShadowSet* sh, const Spill& sp, Counters* cnt) {
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        int st = kAmb;
+        if (!FORCE64) {
+            float at, dt;
+            st = classify(T, O, sh->d32[k], sh->hlo[k], sh->hhi[k], &at, &dt);
+            if (coplanar) st = kMiss;
+        }
+        bool hit = (st == kCand);
+        if (st == kAmb && !sh->occ[k]) {   // rare (FORCE64: always) — f64 decision
+            D3 Q;
+            double sqd;
+            if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
+            const D3 P = sp.get3(kSpP), L = sp.get3(kSpL + 3 * k);
+            hit = eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
+                  sqd < squared_dist(P, L);
+        }
+        if (hit && !sh->occ[k]) {
+            sh->occ[k] = true;
+            sh->first[k] = t + 1;
+            if (k == kLightSamples - 1) sh->leak = S.tri_obj[t];
+        }
+    }
+}
+
+template <bool COUNT>
+PT_HD D3 shadow_color(const SceneK& S, D3 n, int obj, const ShadowSet& sh, const Spill& sp,
+                      Counters* cnt) {
+    double dsum = 0.0;
+    const D3 P = sp.get3(kSpP);
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        if (!sh.occ[k]) dsum += dot(unit(sp.get3(kSpL + 3 * k) - P), n);   // main.py:66-68
+        bump<COUNT>(cnt, &Counters::shadow_tests, (uint32_t)sh.first[k]);
     }
     dsum /= (double)kLightSamples;
     const Mat& m = S.mat[obj];
-    const Mat& lm = S.mat[leak];
+    const Mat& lm = S.mat[sh.leak];
     bump<COUNT>(cnt, &Counters::shading_points, 1);
     return d3(m.rgb[0] * m.ka * S.ambient + S.light_rgb[0] * lm.rgb[0] * dsum,
               m.rgb[1] * m.ka * S.ambient + S.light_rgb[1] * lm.rgb[1] * dsum,
               m.rgb[2] * m.ka * S.ambient + S.light_rgb[2] * lm.rgb[2] * dsum);
+}
+
+// Standalone compute_color (batched API): u = the 12 light-sampling uniforms.
+template <bool FORCE64, bool COUNT>
+PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
+             const Spill& sp, Counters* cnt) {
+    ShadowSet sh;
+    sp.put3(kSpP, P);
+    shadow_setup(S, P, u, 0, 0, 0, 0, &sh, sp);
+    const F3 o32 = to_f3(P - ld3(S.center));
+    for (int t = 0; t < S.n_obj_tri; ++t) {
+        if (PT_WAVE_ALL(sh.occ[0] && sh.occ[1] && sh.occ[2])) break;
+        const TriF T = S.trif[t];
+        const OriginF O = FORCE64 ? OriginF{0.f, 0.f, 0.f} : origin_f(T, o32);
+        shadow_test<FORCE64, COUNT>(S, T, O, t, T.grp == ogrp, &sh, sp, cnt);
+    }
+    return shadow_color<COUNT>(S, n, obj, sh, sp, cnt);
 }
 
 // ---------------------------------------------------------------- bounce --
@@ -172,16 +259,11 @@ PT_HD D3 bounce(const SceneK& S, const TriS& R, const Mat& m, D3 P, D3 d_old,
     const D3 n = ld3(R.n);
     const double xi = 0.0 + (m.kdks - 0.0) * u_sel;
     if (xi <= m.kd) {   // diffuse: phi = arccos(sqrt(u)), theta = 6.28 u
-        const double cphi = sqrt(u_phi);
-        const double sphi = sqrt(1.0 - u_phi);   // sin(arccos(sqrt(u)))
-        const double th = kTau * u_theta;
+        const double cphi = sqrt_d(u_phi);
+        const double sphi = sqrt_d(1.0 - u_phi);   // sin(arccos(sqrt(u)))
+        const double th = kTau * u_theta;          // in [0, 6.28)
         double st, ct;
-#if defined(__HIP_DEVICE_COMPILE__)
-        sincos(th, &st, &ct);
-#else
-        st = sin(th);
-        ct = cos(th);
-#endif
+        sincos_small(th, &st, &ct);
         const D3 nd = rotate_y(R, d3(sphi * ct, sphi * st, cphi));
         *kf = m.kd * dot(nd, n);
         return nd;
@@ -219,8 +301,8 @@ struct LaneJob {
 // sample, main.py:191), so a wave keeps tracing until all its lanes are out
 // of samples.
 template <bool FORCE64, bool COUNT>
-PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 eye, D3 d0, int tri0, D3 P0,
-                     Counters* cnt) {
+PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
+                     const Spill& sp, Counters* cnt) {
     D3 acc = d3(0, 0, 0);
     if (J.n_samples <= 0 || J.bounces <= 0) return acc;   // main.py:192 never runs
     if (tri0 < 0 || tri0 >= S.n_obj_tri) {   // primary ray escapes or hits the light
@@ -239,9 +321,11 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 eye, D3 d0, int tri0,
     int si = 0;
     int b = 0;
     int tri = tri0;
-    D3 P = P0, d = d0, rgb = d3(0, 0, 0);
+    D3 P = P0;
     double k = 1.0;
     bool active = true;
+    sp.put3(kSpD0, d0);
+    sp.put3(kSpNd, d0);   // incoming direction of bounce 0 (main.py:191)
     if (COUNT) {   // the cached primary trace, counted per sample
         bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
         bump<COUNT>(cnt, &Counters::ray_bounces, 1);
@@ -251,49 +335,70 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 eye, D3 d0, int tri0,
         const int obj = S.tri_obj[tri];
         const TriS R = S.tris[tri];
         const Mat& m = S.mat[obj];
-        // direct light at this hit (slots 0..11)
-        double u[12];
-        uint32_t w[4];
-#pragma unroll
-        for (int blk = 0; blk < 3; ++blk) {
-            rng_block(J.seed, J.pixel, sample, (uint32_t)b, (uint32_t)blk, w);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) u[4 * blk + j] = u_of(w[j]);
-        }
         const int ogrp = S.trif[tri].grp;
-        const D3 col = nee<FORCE64, COUNT>(S, P, ld3(R.n), obj, ogrp, u, cnt);
-        rgb = rgb + col * k;   // main.py:230-231
-        // next ray (slots 12..15)
+        // RNG: slots 12..15 (block 3) bounce + RR here; slots 0..11 (blocks
+        // 0..2) light sampling, drawn in shadow_setup
+        uint32_t w[4];
         rng_block(J.seed, J.pixel, sample, (uint32_t)b, 3u, w);
+        // next ray first (main.py:236-268): it does not depend on the colour
         double kf;
-        const D3 nd = bounce(S, R, m, P, d, u_of(w[0]), u_of(w[1]), u_of(w[2]), &kf);
-        k *= kf;
-        bool done = (b + 1 >= J.bounces);
-        if (!done && J.rr_depth >= 0 && b >= J.rr_depth) {   // build extension
-            double q = fabs(k);
+        const D3 nd = bounce(S, R, m, P, sp.get3(kSpNd), u_of(w[0]), u_of(w[1]), u_of(w[2]), &kf);
+        const double kn = k * kf;
+        bool trace = (b + 1 < J.bounces);
+        double kk = kn;
+        if (trace && J.rr_depth >= 0 && b >= J.rr_depth) {   // build extension
+            double q = fabs(kn);
             q = q < 0.05 ? 0.05 : (q > 1.0 ? 1.0 : q);
-            if (u_of(w[3]) >= q) done = true;
-            else k /= q;
+            if (u_of(w[3]) >= q) trace = false;
+            else kk = kn / q;
         }
-        if (!done) {
+        // one pass: 3 shadow rays + the next ray's closest hit, same origin
+        ShadowSet sh;
+        sp.put3(kSpP, P);
+        sp.put3(kSpNd, nd);
+        shadow_setup(S, P, nullptr, J.seed, J.pixel, sample, (uint32_t)b, &sh, sp);
+        const F3 o32 = to_f3(P - ld3(S.center));
+        const F3 n32 = to_f3(unit(nd));
+        ClosestAcc ca = closest_init();
+        const bool any_trace = PT_WAVE_ANY(trace);
+        for (int t = 0; t < S.n_obj_tri; ++t) {
+            const TriF T = S.trif[t];
+            const OriginF O = FORCE64 ? OriginF{0.f, 0.f, 0.f} : origin_f(T, o32);
+            const bool coplanar = (T.grp == ogrp);
+            if (PT_WAVE_ANY(!(sh.occ[0] && sh.occ[1] && sh.occ[2])))
+                shadow_test<FORCE64, COUNT>(S, T, O, t, coplanar, &sh, sp, cnt);
+            if (!FORCE64 && any_trace)
+                closest_test<COUNT>(S, T, O, n32, t, coplanar, sp, kSpP, kSpNd, &ca, cnt);
+        }
+        if (!FORCE64 && any_trace) {
+            for (int t = S.n_obj_tri; t < S.n_tri; ++t) {   // the light's triangles
+                const TriF T = S.trif[t];
+                closest_test<COUNT>(S, T, origin_f(T, o32), n32, t, T.grp == ogrp, sp, kSpP,
+                                    kSpNd, &ca, cnt);
+            }
+        }
+        const D3 col = shadow_color<COUNT>(S, ld3(R.n), obj, sh, sp, cnt);
+        acc = acc + col * k;   // main.py:230-231 (k before this bounce's update)
+        k = kk;
+        bool done = !trace;
+        if (trace) {
             D3 Pn;
-            const int tn = closest<FORCE64, COUNT>(S, P, nd, ogrp, &Pn, cnt);
+            const int tn = closest_finish<FORCE64, COUNT>(S, ca, sp.get3(kSpP),
+                                                          unit(sp.get3(kSpNd)), &Pn, cnt);
             if (tn < 0) {
                 bump<COUNT>(cnt, &Counters::escapes, 1);
                 done = true;
             } else if (tn >= S.n_obj_tri) {   // light: main.py:214-215
-                rgb = rgb + ld3(S.light_rgb) * k;
+                acc = acc + ld3(S.light_rgb) * k;
                 bump<COUNT>(cnt, &Counters::light_hits, 1);
                 done = true;
             } else {
-                d = nd;
                 P = Pn;
                 tri = tn;
                 ++b;
             }
         }
         if (done) {
-            acc = acc + rgb;
             ++si;
             if (si >= J.n_samples) {
                 active = false;
@@ -301,9 +406,8 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 eye, D3 d0, int tri0,
                 b = 0;
                 tri = tri0;
                 P = P0;
-                d = d0;
                 k = 1.0;
-                rgb = d3(0, 0, 0);
+                sp.put3(kSpNd, sp.get3(kSpD0));
                 if (COUNT) {
                     bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
                     bump<COUNT>(cnt, &Counters::ray_bounces, 1);
@@ -311,7 +415,6 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 eye, D3 d0, int tri0,
             }
         }
     }
-    (void)eye;
     return acc;
 }
 

@@ -29,6 +29,8 @@ int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
     int32_t first, rows;
     if (!band_layout(p, &first, &rows)) return -2;
     Counters c = {};
+    double spill_mem[kSpillSlots];
+    const Spill sp{spill_mem, 1};
     for (int r = 0; r < rows; ++r) {
         const int iy = first + r * p->row_step;
         for (int ix = 0; ix < p->width; ++ix) {
@@ -48,11 +50,11 @@ int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
             int tri0 = -1;
             D3 acc;
             if (force64) {
-                if (p->bounces > 0) tri0 = closest<true, false>(H.k, eye, d0, -1, &P0, &c);
-                acc = render_lane<true, true>(H.k, J, eye, d0, tri0, P0, &c);
+                if (p->bounces > 0) tri0 = closest<true, false>(H.k, eye, d0, -1, sp, &P0, &c);
+                acc = render_lane<true, true>(H.k, J, d0, tri0, P0, sp, &c);
             } else {
-                if (p->bounces > 0) tri0 = closest<false, false>(H.k, eye, d0, -1, &P0, &c);
-                acc = render_lane<false, true>(H.k, J, eye, d0, tri0, P0, &c);
+                if (p->bounces > 0) tri0 = closest<false, false>(H.k, eye, d0, -1, sp, &P0, &c);
+                acc = render_lane<false, true>(H.k, J, d0, tri0, P0, sp, &c);
             }
             double* o = out + ((size_t)(rows - 1 - r) * p->width + ix) * 3;
             o[0] = acc.x / p->spp; o[1] = acc.y / p->spp; o[2] = acc.z / p->spp;
