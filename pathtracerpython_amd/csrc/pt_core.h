@@ -37,27 +37,38 @@ constexpr float kTzLo = 0.0031622745f;   // sqrt(1e-5) * (1 - 1e-6)
 constexpr float kTzHi = 0.0031622809f;   // sqrt(1e-5) * (1 + 1e-6)
 
 // ------------------------------------------------------------- records --
-// f32 filter record (80 B, one s_load_dwordx16 + one dwordx4).  Coordinates
-// are relative to SceneK::center.  Forms (x = origin, d = unit direction):
-//   h(x) = n.x + cn      signed distance to the plane (n = reference v_plane)
+// f32 filter records.  Triangles are grouped into plane UNITS: 1 or 2
+// consecutive triangles (scene order, same object) lying in one plane — the
+// reference's quads are such pairs.  Per (ray, unit) the plane part of a test
+// (q = n.d, 1/q, t, the error bound of t, the range checks) is computed once;
+// per triangle only the barycentric part.  Coordinates are relative to
+// SceneK::center.  Forms (x = origin, d = unit direction):
+//   h(x) = n.x + cn      signed distance to the plane (n = reference v_plane
+//                        of the unit's first triangle)
 //   b(x) = gb.x + cb     barycentric weight of v2   (affine, plane-invariant)
 //   c(x) = gc.x + cc     barycentric weight of v3
-// Error constants (see host prepare, pt_scene.cpp):
-//   eh, eq : abs error of h(o) and q = n.d
-//   eo, ed : abs error of b(o)/c(o) and b(d)/c(d) (max of the two)
+// Error constants (host prepare, pt_prepare.h):
+//   eh, eq : abs error of h(o) and of q = n.d (eq also covers the rounding of
+//            1/q and t, and the unit's plane mismatch between its triangles)
+//   eo, ed : abs error of b(o)/c(o) (+ 8u for the weights' own rounding) and
+//            of b(d)/c(d) (max of the two forms)
 //   g      : max(|gb|_1, |gc|_1)
-//   qlo,qhi: |q| below qlo is certainly <= 1e-5 (parallel reject), above qhi
-//            certainly > 1e-5
+//   qhi    : |q| above qhi is certainly > 1e-5 (the reference's parallel test)
 //   grp    : coplanar group (host-verified in f64).  A line whose origin lies
-//            on a triangle of the same group meets this plane at |t| < 1e-3,
+//            on a triangle of the same group meets this plane at |t| < 1e-4,
 //            i.e. squared distance < 1e-5: certainly not a usable hit.
-struct alignas(16) TriF {
-    float n[3], cn;
+struct TriB {            // 12 words
     float gb[3], cb;
     float gc[3], cc;
-    float eh, eq, eo, ed;
-    float g, qlo, qhi;
+    float eo, ed, g;
+    int32_t t;           // triangle index in scene order
+};
+struct alignas(16) UnitF {   // 144 B: two s_load_dwordx16 + one dwordx4
+    float n[3], cn;
+    float eh, eq, qhi;
     int32_t grp;
+    int32_t count, pad0, pad1, pad2;
+    TriB tri[2];
 };
 
 // f64 exact record: the reference's plane normal and edges (utils.py:109-111,
@@ -84,14 +95,16 @@ struct alignas(16) Mat {
 };
 
 struct SceneK {
-    const TriF* trif;
+    const UnitF* unit;          // [n_unit] plane units, object units first
     const TriD* trid;
     const TriS* tris;
     const int32_t* tri_obj;
     const Mat* mat;
     const int32_t* light_tri;   // [n_light] global triangle index
     const double* light_cum;    // [n_light+1] running area sums (utils.py:31-35)
+    const int32_t* tri_grp;     // [n_tri] coplanar group of each triangle
     int32_t n_tri, n_obj_tri, n_obj, n_light;
+    int32_t n_unit, n_obj_unit, pad0, pad1;
     double light_sum;
     double eye[3];
     double ortho[4];
@@ -189,49 +202,40 @@ PT_HD float rcpf(float x) {
 // Filter verdicts
 enum : int { kMiss = 0, kCand = 1, kAmb = 2 };
 
-// Origin-dependent parts of a test, shared by rays with the same origin.
-struct OriginF { float h, bo, co; };
-PT_HD OriginF origin_f(const TriF& T, F3 o) {
-    OriginF r;
-    r.h = aff3(T.n, T.cn, o);
-    r.bo = aff3(T.gb, T.cb, o);
-    r.co = aff3(T.gc, T.cc, o);
-    return r;
+// Plane part of a test (per ray and unit).  Range semantics:
+//   closest: valid iff sqd > 1e-5                 -> hi = inf
+//   shadow : occluder iff 1e-5 <= sqd < |L - P|^2 -> hi_lo/hi_hi bracket tL
+struct RayPlane {
+    float t, at, dt;
+    bool rmiss;    // |t| certainly out of range: the test is a certain miss
+    bool rcand;    // |t| certainly in range and |q| certainly > 1e-5
+};
+PT_HD RayPlane ray_plane(const UnitF& U, float h, F3 d, float hi_lo, float hi_hi) {
+    RayPlane p;
+    const float q = lin3(U.n, d);
+    const float r = rcpf(q);
+    p.t = -h * r;
+    p.at = fabsf(p.t);
+    // |t_ref - t| <= (eh + |t| eq) / |q|  (eq absorbs the 3u|t| of 1/q and t)
+    p.dt = fabsf(r) * fmaf(p.at, U.eq, U.eh);
+    p.rmiss = (p.at + p.dt < kTzLo) | (p.at - p.dt >= hi_hi);
+    p.rcand = (fabsf(q) > U.qhi) & (p.at - p.dt > kTzHi) & (p.at + p.dt < hi_lo);
+    return p;
 }
 
-// Core classification (branch-free: on a 64-lane wave the lanes rarely agree
-// on an early exit, so everything is computed and selected).  Returns kMiss
-// when the reference certainly reports "no intersection usable in range",
-// kCand when it certainly reports an intersection inside the triangle with
-// |t| in range (|t| interval [t-dt, t+dt] returned), kAmb otherwise.
-// Range semantics:
-//   closest: valid iff sqd > 1e-5                 -> hi = inf
-//   shadow : occluder iff 1e-5 <= sqd < |L - P|^2 -> hi = tL (hi_lo/hi_hi
-//            bracket tL with slack)
-PT_HD int classify(const TriF& T, const OriginF& O, F3 d, float hi_lo, float hi_hi,
-                   float* t_abs, float* t_err) {
-    const float q = lin3(T.n, d);
-    const float aq = fabsf(q);
-    const float r = rcpf(q);
-    const float t = -O.h * r;
-    const float at = fabsf(t);
-    const float dt = fmaf(fmaf(at, T.eq, T.eh), fabsf(r), 8.0f * kU * at);
-    const float beta = fmaf(t, lin3(T.gb, d), O.bo);
-    const float gam = fmaf(t, lin3(T.gc, d), O.co);
+// Barycentric part (per ray and triangle): kMiss when the reference certainly
+// reports no usable intersection, kCand when it certainly reports one (|t|
+// in [at - dt, at + dt]), kAmb otherwise.  Branch-free.
+PT_HD int classify_tri(const TriB& B, const RayPlane& p, float bo, float co, F3 d) {
+    const float beta = fmaf(p.t, lin3(B.gb, d), bo);
+    const float gam = fmaf(p.t, lin3(B.gc, d), co);
     const float alpha = (1.0f - beta) - gam;
-    // |beta_ref - beta| <= del2, |gamma_ref - gamma| <= del2,
-    // |alpha_ref - alpha| <= 2*del2 (alpha = 1 - beta - gamma, two roundings)
-    const float del2 = fmaf(T.g, dt, fmaf(at, T.ed, T.eo)) + 8.0f * kU;
-    // certainly a miss: |dot| certainly <= 1e-5 (parallel reject), or a
-    // weight certainly negative, or |P - o|^2 certainly < 1e-5, or certainly
-    // beyond the range
-    const bool miss = (aq < T.qlo) | (min3f(beta, gam, alpha + del2) < -del2) |
-                      (at + dt < kTzLo) | (at - dt >= hi_hi);
-    const bool cand = (aq > T.qhi) & (min3f(beta, gam, alpha - del2) > del2) &
-                      (at - dt > kTzHi) & (at + dt < hi_lo);
-    *t_abs = at;
-    *t_err = dt;
-    return miss ? kMiss : (cand ? kCand : kAmb);
+    // |beta_ref - beta| <= del, |gamma_ref - gamma| <= del,
+    // |alpha_ref - alpha| <= 2 del (eo carries the 8u rounding slack)
+    const float del = fmaf(B.g, p.dt, fmaf(p.at, B.ed, B.eo));
+    const bool out = min3f(beta, gam, alpha + del) < -del;
+    const bool in = min3f(beta, gam, alpha - del) > del;
+    return (p.rmiss | out) ? kMiss : ((p.rcand & in) ? kCand : kAmb);
 }
 
 // ------------------------------------------------------ light sampling --

@@ -254,18 +254,21 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         return fail(PT_ENODEV, "device is " + arch + ", this build targets gfx950 only");
     }
     HostScene& H = s->host;
-    const size_t sz[7] = {H.trif.size() * sizeof(TriF), H.trid.size() * sizeof(TriD),
-                          H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
-                          H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
-                          H.light_cum.size() * sizeof(double)};
-    const void* src[7] = {H.trif.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
-                          H.mat.data(), H.light_tri.data(), H.light_cum.data()};
-    size_t off[7], total = 0;
-    for (int i = 0; i < 7; ++i) { off[i] = total; total += align_up(sz[i]); }
+    constexpr int kArrays = 8;
+    const size_t sz[kArrays] = {H.unit.size() * sizeof(UnitF), H.trid.size() * sizeof(TriD),
+                                H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
+                                H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
+                                H.light_cum.size() * sizeof(double),
+                                H.tri_grp.size() * sizeof(int32_t)};
+    const void* src[kArrays] = {H.unit.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
+                                H.mat.data(), H.light_tri.data(), H.light_cum.data(),
+                                H.tri_grp.data()};
+    size_t off[kArrays], total = 0;
+    for (int i = 0; i < kArrays; ++i) { off[i] = total; total += align_up(sz[i]); }
     int rc = PT_OK;
     auto cleanup = [&](int code, const std::string& m) { pt_scene_destroy(s); return fail(code, m); };
     if (hipMalloc(&s->blob, total) != hipSuccess) return cleanup(PT_ENOMEM, "hipMalloc scene tables");
-    for (int i = 0; i < 7; ++i)
+    for (int i = 0; i < kArrays; ++i)
         if (hipMemcpy((char*)s->blob + off[i], src[i], sz[i], hipMemcpyHostToDevice) != hipSuccess)
             return cleanup(PT_EHIP, "hipMemcpy scene tables");
     if (hipMalloc((void**)&s->stats, sizeof(StatsDev)) != hipSuccess) return cleanup(PT_ENOMEM, "hipMalloc stats");
@@ -274,13 +277,14 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         return cleanup(PT_EHIP, "stream/event creation");
     s->dev = H.k;
     char* b = (char*)s->blob;
-    s->dev.trif = (const TriF*)(b + off[0]);
+    s->dev.unit = (const UnitF*)(b + off[0]);
     s->dev.trid = (const TriD*)(b + off[1]);
     s->dev.tris = (const TriS*)(b + off[2]);
     s->dev.tri_obj = (const int32_t*)(b + off[3]);
     s->dev.mat = (const Mat*)(b + off[4]);
     s->dev.light_tri = (const int32_t*)(b + off[5]);
     s->dev.light_cum = (const double*)(b + off[6]);
+    s->dev.tri_grp = (const int32_t*)(b + off[7]);
     s->xbound = box_bound(H);
     *out = s;
     return rc;

@@ -68,26 +68,52 @@ PT_HD void closest_add(ClosestAcc* c, int t, float a, float b) {
     else { c->a2 = fminf(c->a2, a); }
 }
 
+// Origin terms of a unit (shared by every ray from the same origin): the
+// plane distance and each triangle's barycentric forms at the origin.
+struct OriginU { float h, bo0, co0, bo1, co1; };
+PT_HD OriginU origin_u(const UnitF& U, F3 o) {
+    OriginU r;
+    r.h = aff3(U.n, U.cn, o);
+    r.bo0 = aff3(U.tri[0].gb, U.tri[0].cb, o);
+    r.co0 = aff3(U.tri[0].gc, U.tri[0].cc, o);
+    r.bo1 = r.co1 = 0.f;
+    if (U.count == 2) {   // wave-uniform
+        r.bo1 = aff3(U.tri[1].gb, U.tri[1].cb, o);
+        r.co1 = aff3(U.tri[1].gc, U.tri[1].cc, o);
+    }
+    return r;
+}
+
 template <bool COUNT>
-PT_HD void closest_test(const SceneK& S, const TriF& T, const OriginF& O, F3 d32, int t,
-                        bool coplanar, const Spill& sp, int o_slot, int dn_slot,
-                        ClosestAcc* acc, Counters* cnt) {
-    float at = 0.f, dt = 0.f;
-    int st = classify(T, O, d32, INFINITY, INFINITY, &at, &dt);
+PT_HD void closest_tri(const SceneK& S, const TriB& B, const RayPlane& p, float bo, float co,
+                       F3 d32, bool coplanar, const Spill& sp, int o_slot, int dn_slot,
+                       ClosestAcc* acc, Counters* cnt) {
+    int st = classify_tri(B, p, bo, co, d32);
     if (coplanar) st = kMiss;
-    float a = (st == kCand) ? at - dt : INFINITY;
-    float b = (st == kCand) ? at + dt : INFINITY;
+    float a = (st == kCand) ? p.at - p.dt : INFINITY;
+    float b = (st == kCand) ? p.at + p.dt : INFINITY;
     if (st == kAmb) {   // rare: decide this test in f64
         D3 Q;
         double sqd;
         bump<COUNT>(cnt, &Counters::fallbacks, 1);
-        if (eval64(S.trid[t], sp.get3(o_slot), unit(sp.get3(dn_slot)), &Q, &sqd) && sqd > kZero) {
-            const float s = sqrtf((float)sqd);   // |t| to ~1e-7; brackets are 1e-6
-            a = s * (1.0f - 1e-6f);
-            b = s * (1.0f + 1e-6f);
+        if (eval64(S.trid[B.t], sp.get3(o_slot), unit(sp.get3(dn_slot)), &Q, &sqd) && sqd > kZero) {
+            const float sq = sqrtf((float)sqd);   // |t| to ~1e-7; brackets are 1e-6
+            a = sq * (1.0f - 1e-6f);
+            b = sq * (1.0f + 1e-6f);
         }
     }
-    closest_add(acc, t, a, b);
+    closest_add(acc, B.t, a, b);
+}
+
+// One closest-hit ray against one plane unit.
+template <bool COUNT>
+PT_HD void closest_unit(const SceneK& S, const UnitF& U, const OriginU& O, F3 d32, bool coplanar,
+                        const Spill& sp, int o_slot, int dn_slot, ClosestAcc* acc,
+                        Counters* cnt) {
+    const RayPlane p = ray_plane(U, O.h, d32, INFINITY, INFINITY);
+    closest_tri<COUNT>(S, U.tri[0], p, O.bo0, O.co0, d32, coplanar, sp, o_slot, dn_slot, acc, cnt);
+    if (U.count == 2)
+        closest_tri<COUNT>(S, U.tri[1], p, O.bo1, O.co1, d32, coplanar, sp, o_slot, dn_slot, acc, cnt);
 }
 
 // Finish a closest-hit query: the candidate with the smallest lower bound is
@@ -132,9 +158,9 @@ PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, const Spill& sp, D3* P,
         sp.put3(kSpNd, d);
         const F3 o32 = to_f3(o - ld3(S.center));
         const F3 d32 = to_f3(dn);
-        for (int t = 0; t < S.n_tri; ++t) {
-            const TriF T = S.trif[t];
-            closest_test<COUNT>(S, T, origin_f(T, o32), d32, t, T.grp == ogrp, sp, kSpP, kSpNd,
+        for (int u = 0; u < S.n_unit; ++u) {
+            const UnitF U = S.unit[u];
+            closest_unit<COUNT>(S, U, origin_u(U, o32), d32, U.grp == ogrp, sp, kSpP, kSpNd,
                                 &acc, cnt);
         }
     }
@@ -187,30 +213,39 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, u
 }
 
 template <bool FORCE64, bool COUNT>
-PT_HD void shadow_test(const SceneK& S, const TriF& T, const OriginF& O, int t, bool coplanar,
+PT_HD void shadow_tri(const SceneK& S, const TriB& B, int k, int st, ShadowSet* sh,
+                      const Spill& sp, Counters* cnt) {
+    bool hit = (st == kCand);
+    if (st == kAmb && !sh->occ[k]) {   // rare (FORCE64: always) — f64 decision
+        D3 Q;
+        double sqd;
+        if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
+        const D3 P = sp.get3(kSpP), L = sp.get3(kSpL + 3 * k);
+        hit = eval64(S.trid[B.t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
+              sqd < squared_dist(P, L);
+    }
+    if (hit && !sh->occ[k]) {
+        sh->occ[k] = true;
+        sh->first[k] = B.t + 1;
+        if (k == kLightSamples - 1) sh->leak = S.tri_obj[B.t];
+    }
+}
+
+// The 3 shadow rays against one plane unit, triangles in scene order.
+template <bool FORCE64, bool COUNT>
+PT_HD void shadow_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
                        ShadowSet* sh, const Spill& sp, Counters* cnt) {
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
-        int st = kAmb;
+        int st0 = kAmb, st1 = kAmb;
         if (!FORCE64) {
-            float at, dt;
-            st = classify(T, O, sh->d32[k], sh->hlo[k], sh->hhi[k], &at, &dt);
-            if (coplanar) st = kMiss;
+            const RayPlane p = ray_plane(U, O.h, sh->d32[k], sh->hlo[k], sh->hhi[k]);
+            st0 = coplanar ? kMiss : classify_tri(U.tri[0], p, O.bo0, O.co0, sh->d32[k]);
+            if (U.count == 2)
+                st1 = coplanar ? kMiss : classify_tri(U.tri[1], p, O.bo1, O.co1, sh->d32[k]);
         }
-        bool hit = (st == kCand);
-        if (st == kAmb && !sh->occ[k]) {   // rare (FORCE64: always) — f64 decision
-            D3 Q;
-            double sqd;
-            if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
-            const D3 P = sp.get3(kSpP), L = sp.get3(kSpL + 3 * k);
-            hit = eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
-                  sqd < squared_dist(P, L);
-        }
-        if (hit && !sh->occ[k]) {
-            sh->occ[k] = true;
-            sh->first[k] = t + 1;
-            if (k == kLightSamples - 1) sh->leak = S.tri_obj[t];
-        }
+        shadow_tri<FORCE64, COUNT>(S, U.tri[0], k, st0, sh, sp, cnt);
+        if (U.count == 2) shadow_tri<FORCE64, COUNT>(S, U.tri[1], k, st1, sh, sp, cnt);
     }
 }
 
@@ -241,11 +276,11 @@ PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
     sp.put3(kSpP, P);
     shadow_setup(S, P, u, 0, 0, 0, 0, &sh, sp);
     const F3 o32 = to_f3(P - ld3(S.center));
-    for (int t = 0; t < S.n_obj_tri; ++t) {
+    for (int u = 0; u < S.n_obj_unit; ++u) {
         if (PT_WAVE_ALL(sh.occ[0] && sh.occ[1] && sh.occ[2])) break;
-        const TriF T = S.trif[t];
-        const OriginF O = FORCE64 ? OriginF{0.f, 0.f, 0.f} : origin_f(T, o32);
-        shadow_test<FORCE64, COUNT>(S, T, O, t, T.grp == ogrp, &sh, sp, cnt);
+        const UnitF U = S.unit[u];
+        const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
+        shadow_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, &sh, sp, cnt);
     }
     return shadow_color<COUNT>(S, n, obj, sh, sp, cnt);
 }
@@ -335,7 +370,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         const int obj = S.tri_obj[tri];
         const TriS R = S.tris[tri];
         const Mat& m = S.mat[obj];
-        const int ogrp = S.trif[tri].grp;
+        const int ogrp = S.tri_grp[tri];
         // RNG: slots 12..15 (block 3) bounce + RR here; slots 0..11 (blocks
         // 0..2) light sampling, drawn in shadow_setup
         uint32_t w[4];
@@ -361,20 +396,20 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         const F3 n32 = to_f3(unit(nd));
         ClosestAcc ca = closest_init();
         const bool any_trace = PT_WAVE_ANY(trace);
-        for (int t = 0; t < S.n_obj_tri; ++t) {
-            const TriF T = S.trif[t];
-            const OriginF O = FORCE64 ? OriginF{0.f, 0.f, 0.f} : origin_f(T, o32);
-            const bool coplanar = (T.grp == ogrp);
+        for (int u = 0; u < S.n_obj_unit; ++u) {
+            const UnitF U = S.unit[u];
+            const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
+            const bool coplanar = (U.grp == ogrp);
             if (PT_WAVE_ANY(!(sh.occ[0] && sh.occ[1] && sh.occ[2])))
-                shadow_test<FORCE64, COUNT>(S, T, O, t, coplanar, &sh, sp, cnt);
+                shadow_unit<FORCE64, COUNT>(S, U, O, coplanar, &sh, sp, cnt);
             if (!FORCE64 && any_trace)
-                closest_test<COUNT>(S, T, O, n32, t, coplanar, sp, kSpP, kSpNd, &ca, cnt);
+                closest_unit<COUNT>(S, U, O, n32, coplanar, sp, kSpP, kSpNd, &ca, cnt);
         }
         if (!FORCE64 && any_trace) {
-            for (int t = S.n_obj_tri; t < S.n_tri; ++t) {   // the light's triangles
-                const TriF T = S.trif[t];
-                closest_test<COUNT>(S, T, origin_f(T, o32), n32, t, T.grp == ogrp, sp, kSpP,
-                                    kSpNd, &ca, cnt);
+            for (int u = S.n_obj_unit; u < S.n_unit; ++u) {   // the light's units
+                const UnitF U = S.unit[u];
+                closest_unit<COUNT>(S, U, origin_u(U, o32), n32, U.grp == ogrp, sp, kSpP, kSpNd,
+                                    &ca, cnt);
             }
         }
         const D3 col = shadow_color<COUNT>(S, ld3(R.n), obj, sh, sp, cnt);

@@ -17,7 +17,8 @@
 namespace pt {
 
 struct HostScene {
-    std::vector<TriF> trif;
+    std::vector<UnitF> unit;
+    std::vector<int32_t> tri_grp;
     std::vector<TriD> trid;
     std::vector<TriS> tris;
     std::vector<int32_t> tri_obj;
@@ -84,69 +85,63 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     X = X * 1.001 + 1e-6;
     const double u = 1.0 / 16777216.0;   // f32 unit roundoff
 
-    H->trif.assign(T, TriF{});
     H->trid.assign(T, TriD{});
     H->tris.assign(T, TriS{});
     H->tri_obj.assign(d->tri_obj, d->tri_obj + T);
+    // per-triangle f32 filter data, before grouping into units
+    struct PlaneD { double n[3], cn, eh, eq; bool ok; };
+    std::vector<PlaneD> pl(T);
+    std::vector<TriB> tb(T);
+    const D3 Cd = d3(C[0], C[1], C[2]);
+    auto l1 = [](double a, double b, double c) { return fabs(a) + fabs(b) + fabs(c); };
+    const double s = 1.25;   // safety factor over the first-order bounds below
     for (int t = 0; t < T; ++t) {
         const D3 v1 = tri_vertex(d, t, 0), v2 = tri_vertex(d, t, 1), v3 = tri_vertex(d, t, 2);
         TriD& E = H->trid[t];
         // reference plane normal: normalize(cross(v1 - v2, v3 - v2)), utils.py:109-111
         const D3 cr = cross(v1 - v2, v3 - v2);
         const double cn = sqrt(dot(cr, cr));
-        const D3 vp = cr * (1.0 / cn);
         E.vp[0] = cr.x / cn; E.vp[1] = cr.y / cn; E.vp[2] = cr.z / cn;  // v / norm(v)
         E.cvp = E.vp[0] * v1.x + E.vp[1] * v1.y + E.vp[2] * v1.z;
         const D3 e12 = v1 - v2, e23 = v2 - v3, e31 = v3 - v1;
         const double* src[6] = {&v1.x, &v2.x, &v3.x, &e12.x, &e23.x, &e31.x};
         double* dst[6] = {E.v1, E.v2, E.v3, E.e12, E.e23, E.e31};
         for (int j = 0; j < 6; ++j) memcpy(dst[j], src[j], 3 * sizeof(double));
-        (void)vp;
 
         TriS& R = H->tris[t];
         memcpy(R.n, d->tri_n + 3 * t, 3 * sizeof(double));
         rotation_for_normal(R.n, &R);
 
-        // f32 filter record in centred coordinates
-        TriF& F = H->trif[t];
-        const D3 Cd = d3(C[0], C[1], C[2]);
+        // f32 filter data in centred coordinates
         const D3 w1 = v1 - Cd, w2 = v2 - Cd, w3 = v3 - Cd;
         const D3 e1 = w2 - w1, e2 = w3 - w1, N = cross(e1, e2);
         const double NN = dot(N, N);
-        if (!(cn > 0.0) || !(NN > 0.0) || !isfinite(cn)) {
-            // degenerate: the reference's NaN normal fails |dot| > 1e-5 -> always miss
-            F.qlo = INFINITY;
-            F.qhi = INFINITY;
-            continue;
-        }
+        PlaneD& P = pl[t];
+        TriB& B = tb[t];
+        B = TriB{};
+        B.t = t;
+        P.ok = (cn > 0.0) && (NN > 0.0) && isfinite(cn);
+        if (!P.ok) continue;   // degenerate: the reference's NaN normal never hits
         const D3 gb = cross(e2, N) * (1.0 / NN), gc = cross(N, e1) * (1.0 / NN);
         const double cb = -dot(gb, w1), cc = -dot(gc, w1);
         const double chn = -(E.vp[0] * w1.x + E.vp[1] * w1.y + E.vp[2] * w1.z);
-        F.n[0] = (float)E.vp[0]; F.n[1] = (float)E.vp[1]; F.n[2] = (float)E.vp[2];
-        F.cn = (float)chn;
-        F.gb[0] = (float)gb.x; F.gb[1] = (float)gb.y; F.gb[2] = (float)gb.z; F.cb = (float)cb;
-        F.gc[0] = (float)gc.x; F.gc[1] = (float)gc.y; F.gc[2] = (float)gc.z; F.cc = (float)cc;
-        // bounds: an f32 affine form g.x + c at |x_i| <= X, evaluated as an
-        // fma chain from rounded inputs, errs by <= 5u(|g|_1 X + |c|) (input
-        // and coefficient rounding 2u|g|_1 X + u|c|, three fmas 3u(...)); we
-        // use 8u and a further 1.25x for second-order terms.
-        auto l1 = [](double a, double b, double c) { return fabs(a) + fabs(b) + fabs(c); };
-        const double n1 = l1(F.n[0], F.n[1], F.n[2]) * (1 + 4 * u);
-        const double gb1 = l1(F.gb[0], F.gb[1], F.gb[2]) * (1 + 4 * u);
-        const double gc1 = l1(F.gc[0], F.gc[1], F.gc[2]) * (1 + 4 * u);
-        const double s = 1.25;
-        const double eh = s * 8 * u * (n1 * X + fabs(chn));
-        const double eq = s * 8 * u * n1;
-        const double eo = s * (8 * u * std::max(gb1 * X + fabs(cb), gc1 * X + fabs(cc))) + 4 * u;
-        const double ed = s * 8 * u * std::max(gb1, gc1);
-        F.eh = f32_up(eh);
-        F.eq = f32_up(eq);
-        F.eo = f32_up(eo);
-        F.ed = f32_up(ed);
-        F.g = f32_up(std::max(gb1, gc1) * (1 + 1e-3));
-        F.qlo = (float)((1e-5 - eq) * (1 - 1e-4));
-        if (!(F.qlo > 0.f)) F.qlo = 0.f;
-        F.qhi = f32_up((1e-5 + eq) * (1 + 1e-4));
+        for (int i = 0; i < 3; ++i) P.n[i] = E.vp[i];
+        P.cn = chn;
+        B.gb[0] = (float)gb.x; B.gb[1] = (float)gb.y; B.gb[2] = (float)gb.z; B.cb = (float)cb;
+        B.gc[0] = (float)gc.x; B.gc[1] = (float)gc.y; B.gc[2] = (float)gc.z; B.cc = (float)cc;
+        // An f32 affine form g.x + c at |x_i| <= X, evaluated as an fma chain
+        // from rounded inputs, errs by <= 5u(|g|_1 X + |c|) (input and
+        // coefficient rounding 2u|g|_1 X + u|c|, three fmas 3u(...)); we take
+        // 8u, times the safety factor s.  Direction forms: |d_i| <= 1.
+        const double n1 = l1((float)P.n[0], (float)P.n[1], (float)P.n[2]) * (1 + 4 * u);
+        const double gb1 = l1(B.gb[0], B.gb[1], B.gb[2]) * (1 + 4 * u);
+        const double gc1 = l1(B.gc[0], B.gc[1], B.gc[2]) * (1 + 4 * u);
+        P.eh = s * 8 * u * (n1 * X + fabs(chn));
+        // q's own error, plus 8u n1 >= 8u|q| covering the rounding of 1/q and t
+        P.eq = s * 8 * u * n1 + 8 * u * n1;
+        B.eo = f32_up(s * 8 * u * std::max(gb1 * X + fabs(cb), gc1 * X + fabs(cc)) + 8 * u);
+        B.ed = f32_up(s * 8 * u * std::max(gb1, gc1));
+        B.g = f32_up(std::max(gb1, gc1) * (1 + 1e-3));
     }
     // coplanar groups: triangle t joins the group of an earlier
     // representative r when every vertex of t lies within 1e-12 of r's plane
@@ -157,6 +152,7 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     // reject fires): squared distance < 1e-5, never a usable hit.  Candidate
     // representatives are found by hashing the quantised plane; a missed
     // grouping only costs speed, never correctness.
+    H->tri_grp.assign(T, -1);
     {
         std::unordered_map<uint64_t, std::vector<int>> buckets;
         int n_groups = 0;
@@ -166,9 +162,9 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
             return fabs(P.vp[0] * x.x + P.vp[1] * x.y + P.vp[2] * x.z - P.cvp);
         };
         for (int t = 0; t < T; ++t) {
-            TriF& F = H->trif[t];
-            F.grp = -2 - t;   // unique, never equal to an origin's -1
-            if (!(F.qlo < INFINITY)) continue;   // degenerate
+            int32_t& G = H->tri_grp[t];
+            G = -2 - t;   // unique, never equal to an origin's -1
+            if (!pl[t].ok) continue;   // degenerate
             const TriD& E = H->trid[t];
             double k[4] = {E.vp[0], E.vp[1], E.vp[2], E.cvp};
             // canonical sign: first significant normal component positive
@@ -185,14 +181,54 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
                 for (int v = 0; v < 3 && ok; ++v)
                     ok = plane_dist(r, tri_vertex(d, t, v)) <= 1e-12 &&
                          plane_dist(t, tri_vertex(d, r, v)) <= 1e-12;
-                if (ok) { F.grp = H->trif[r].grp; break; }
+                if (ok) { G = H->tri_grp[r]; break; }
             }
-            if (F.grp < 0) {
-                F.grp = n_groups++;
+            if (G < 0) {
+                G = n_groups++;
                 reps.push_back(t);
             }
         }
     }
+    // plane units: consecutive triangles of one object in one coplanar group
+    // share a unit (at most 2).  The unit's plane is its first triangle's; the
+    // members' planes agree to 1e-12 over the box, covered by +1e-9 slack.
+    H->unit.clear();
+    for (int part = 0; part < 2; ++part) {
+        const int t_begin = part == 0 ? 0 : d->n_obj_tri, t_end = part == 0 ? d->n_obj_tri : T;
+        for (int t = t_begin; t < t_end;) {
+            UnitF U{};
+            const PlaneD& P = pl[t];
+            const bool pair = (t + 1 < t_end) && P.ok && pl[t + 1].ok &&
+                              H->tri_grp[t] >= 0 && H->tri_grp[t + 1] == H->tri_grp[t] &&
+                              d->tri_obj[t + 1] == d->tri_obj[t];
+            U.count = pair ? 2 : 1;
+            U.grp = H->tri_grp[t];
+            U.tri[0] = tb[t];
+            U.tri[1] = pair ? tb[t + 1] : TriB{};
+            if (!P.ok) {   // degenerate: dt = -inf -> certain miss, never a candidate
+                U.eh = -INFINITY;
+                U.eq = 0.f;
+                U.qhi = INFINITY;
+            } else {
+                double eh = P.eh, eq = P.eq;
+                if (pair) {
+                    eh = std::max(eh, pl[t + 1].eh) + 1e-9;
+                    eq = std::max(eq, pl[t + 1].eq) + 1e-9;
+                    U.tri[0].eo = f32_up(U.tri[0].eo + 1e-9);
+                    U.tri[1].eo = f32_up(U.tri[1].eo + 1e-9);
+                }
+                for (int i = 0; i < 3; ++i) U.n[i] = (float)P.n[i];
+                U.cn = (float)P.cn;
+                U.eh = f32_up(eh);
+                U.eq = f32_up(eq);
+                U.qhi = f32_up((1e-5 + eq) * (1 + 1e-4));
+            }
+            H->unit.push_back(U);
+            t += U.count;
+        }
+        if (part == 0) H->k.n_obj_unit = (int32_t)H->unit.size();
+    }
+    H->k.n_unit = (int32_t)H->unit.size();
     // materials
     H->mat.assign(d->n_obj, Mat{});
     for (int o = 0; o < d->n_obj; ++o) {
@@ -231,7 +267,8 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
 
 // host pointers (for the host-side check build)
 inline void bind_host(HostScene* H) {
-    H->k.trif = H->trif.data();
+    H->k.unit = H->unit.data();
+    H->k.tri_grp = H->tri_grp.data();
     H->k.trid = H->trid.data();
     H->k.tris = H->tris.data();
     H->k.tri_obj = H->tri_obj.data();

@@ -100,29 +100,34 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
         const F3 o32 = to_f3(o - C), d32 = to_f3(dn);
         const double lim = 0.5 + 40.0 * U(rng);   // a shadow range
         const float hlo = (float)(sqrt(lim) * (1 - 1e-6)), hhi = (float)(sqrt(lim) * (1 + 1e-6));
-        for (int t = 0; t < H.k.n_tri; ++t) {
-            const TriF& T = H.trif[t];
-            const OriginF O = origin_f(T, o32);
-            D3 Q; double sqd;
-            const bool h = eval64(H.trid[t], o, dn, &Q, &sqd);
-            // closest semantics
-            float at = 0, dt = 0;
-            int st = classify(T, O, d32, INFINITY, INFINITY, &at, &dt);
-            const bool ref_c = h && sqd > kZero;
-            ++tests;
-            if (st == kAmb) ++amb;
-            else if ((st == kCand) != ref_c) ++wrong;
-            else if (st == kCand) {
-                ++cand;
-                const double s = sqrt(sqd);
-                if (s < (double)at - dt || s > (double)at + dt) ++wrong;   // interval must cover
+        for (int u = 0; u < H.k.n_unit; ++u) {
+            const UnitF& U = H.unit[u];
+            const OriginU O = origin_u(U, o32);
+            const RayPlane pc = ray_plane(U, O.h, d32, INFINITY, INFINITY);
+            const RayPlane ps = ray_plane(U, O.h, d32, hlo, hhi);
+            for (int i = 0; i < U.count; ++i) {
+                const TriB& B = U.tri[i];
+                const float bo = i ? O.bo1 : O.bo0, co = i ? O.co1 : O.co0;
+                D3 Q; double sqd;
+                const bool h = eval64(H.trid[B.t], o, dn, &Q, &sqd);
+                // closest semantics
+                int st = classify_tri(B, pc, bo, co, d32);
+                const bool ref_c = h && sqd > kZero;
+                ++tests;
+                if (st == kAmb) ++amb;
+                else if ((st == kCand) != ref_c) ++wrong;
+                else if (st == kCand) {
+                    ++cand;
+                    const double sq = sqrt(sqd);   // the |t| interval must cover the truth
+                    if (sq < (double)pc.at - pc.dt || sq > (double)pc.at + pc.dt) ++wrong;
+                }
+                // shadow semantics
+                st = classify_tri(B, ps, bo, co, d32);
+                const bool ref_s = h && !(sqd < kZero) && sqd < lim;
+                ++tests;
+                if (st == kAmb) ++amb;
+                else if ((st == kCand) != ref_s) ++wrong;
             }
-            // shadow semantics
-            st = classify(T, O, d32, hlo, hhi, &at, &dt);
-            const bool ref_s = h && !(sqd < kZero) && sqd < lim;
-            ++tests;
-            if (st == kAmb) ++amb;
-            else if ((st == kCand) != ref_s) ++wrong;
         }
     }
     out[0] = wrong; out[1] = amb; out[2] = tests; out[3] = cand;
