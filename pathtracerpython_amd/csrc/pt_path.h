@@ -249,6 +249,88 @@ PT_HD void shadow_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool c
     }
 }
 
+// One plane unit against the 3 shadow rays and the next ray's closest hit,
+// all from the same origin (the fused per-bounce pass).  Every verdict is
+// computed branch-free; ambiguous tests are only recorded as bits and
+// decided in f64 in one (rare) block per unit, so the common path carries no
+// per-test exec-mask juggling.  Scene order is kept where it matters: for
+// each shadow ray the unit's triangles are decided in order, and both
+// triangles of a unit belong to one object, so the leaked colour of
+// main.py:70 (object of the first occluder) does not depend on which of the
+// two decided first.
+template <bool FORCE64, bool COUNT>
+PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
+                      bool do_shadow, bool do_closest, ShadowSet* sh, F3 n32, ClosestAcc* ca,
+                      const Spill& sp, Counters* cnt) {
+    uint32_t amb = 0;   // bit 2k+i: shadow ray k / triangle i; bit 6+i: closest / triangle i
+    const bool two = (U.count == 2);
+    bool occ0[kLightSamples];
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) occ0[k] = sh->occ[k];
+    if (do_shadow) {
+#pragma unroll
+        for (int k = 0; k < kLightSamples; ++k) {
+            int st0 = kAmb, st1 = kAmb;
+            if (!FORCE64) {
+                const RayPlane p = ray_plane(U, O.h, sh->d32[k], sh->hlo[k], sh->hhi[k]);
+                st0 = coplanar ? kMiss : classify_tri(U.tri[0], p, O.bo0, O.co0, sh->d32[k]);
+                st1 = (coplanar || !two) ? kMiss : classify_tri(U.tri[1], p, O.bo1, O.co1, sh->d32[k]);
+            } else if (!two) {
+                st1 = kMiss;
+            }
+            const bool c0 = (st0 == kCand), c1 = (st1 == kCand);
+            if (COUNT && !occ0[k] && (c0 || c1)) sh->first[k] = (c0 ? U.tri[0].t : U.tri[1].t) + 1;
+            if (k == kLightSamples - 1 && !occ0[k] && (c0 || c1)) sh->leak = S.tri_obj[U.tri[0].t];
+            sh->occ[k] = occ0[k] || c0 || c1;
+            if (!occ0[k]) amb |= ((st0 == kAmb) ? 1u : 0u) << (2 * k) | ((st1 == kAmb) ? 2u : 0u) << (2 * k);
+        }
+    }
+    if (!FORCE64 && do_closest) {
+        const RayPlane p = ray_plane(U, O.h, n32, INFINITY, INFINITY);
+        int st0 = coplanar ? kMiss : classify_tri(U.tri[0], p, O.bo0, O.co0, n32);
+        int st1 = (coplanar || !two) ? kMiss : classify_tri(U.tri[1], p, O.bo1, O.co1, n32);
+        // both candidates of one unit cannot happen (a point certainly inside
+        // one triangle is certainly outside its coplanar neighbour)
+        const bool c = (st0 == kCand) || (st1 == kCand);
+        closest_add(ca, (st0 == kCand) ? U.tri[0].t : U.tri[1].t, c ? p.at - p.dt : INFINITY,
+                    c ? p.at + p.dt : INFINITY);
+        amb |= ((st0 == kAmb) ? 64u : 0u) | ((st1 == kAmb) ? 128u : 0u);
+    }
+    if (amb) {   // rare (FORCE64: every shadow test) — decide in f64
+        const D3 P = sp.get3(kSpP);
+        for (int k = 0; k < kLightSamples; ++k) {
+            for (int i = 0; i < 2; ++i) {
+                if (!((amb >> (2 * k + i)) & 1u)) continue;
+                const int t = U.tri[i].t;
+                D3 Q;
+                double sqd;
+                if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
+                const D3 L = sp.get3(kSpL + 3 * k);
+                if (eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
+                    sqd < squared_dist(P, L)) {
+                    if (COUNT && (!sh->occ[k] || t + 1 < sh->first[k])) sh->first[k] = t + 1;
+                    if (k == kLightSamples - 1) sh->leak = S.tri_obj[t];
+                    sh->occ[k] = true;
+                }
+            }
+        }
+        for (int i = 0; i < 2; ++i) {
+            if (!((amb >> (6 + i)) & 1u)) continue;
+            const int t = U.tri[i].t;
+            D3 Q;
+            double sqd;
+            bump<COUNT>(cnt, &Counters::fallbacks, 1);
+            float a = INFINITY, b = INFINITY;
+            if (eval64(S.trid[t], P, unit(sp.get3(kSpNd)), &Q, &sqd) && sqd > kZero) {
+                const float sq = sqrtf((float)sqd);   // |t| to ~1e-7; brackets are 1e-6
+                a = sq * (1.0f - 1e-6f);
+                b = sq * (1.0f + 1e-6f);
+            }
+            closest_add(ca, t, a, b);
+        }
+    }
+}
+
 template <bool COUNT>
 PT_HD D3 shadow_color(const SceneK& S, D3 n, int obj, const ShadowSet& sh, const Spill& sp,
                       Counters* cnt) {
@@ -399,11 +481,9 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         for (int u = 0; u < S.n_obj_unit; ++u) {
             const UnitF U = S.unit[u];
             const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
-            const bool coplanar = (U.grp == ogrp);
-            if (PT_WAVE_ANY(!(sh.occ[0] && sh.occ[1] && sh.occ[2])))
-                shadow_unit<FORCE64, COUNT>(S, U, O, coplanar, &sh, sp, cnt);
-            if (!FORCE64 && any_trace)
-                closest_unit<COUNT>(S, U, O, n32, coplanar, sp, kSpP, kSpNd, &ca, cnt);
+            const bool do_shadow = PT_WAVE_ANY(!(sh.occ[0] && sh.occ[1] && sh.occ[2]));
+            fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
+                                       &ca, sp, cnt);
         }
         if (!FORCE64 && any_trace) {
             for (int u = S.n_obj_unit; u < S.n_unit; ++u) {   // the light's units
