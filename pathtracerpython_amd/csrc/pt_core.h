@@ -50,9 +50,10 @@ constexpr float kTzHi = 0.0031622809f;   // sqrt(1e-5) * (1 + 1e-6)
 // Error constants (host prepare, pt_prepare.h):
 //   eh, eq : abs error of h(o) and of q = n.d (eq also covers the rounding of
 //            1/q and t, and the unit's plane mismatch between its triangles)
-//   eo, ed : abs error of b(o)/c(o) (+ 8u for the weights' own rounding) and
-//            of b(d)/c(d) (max of the two forms)
-//   g      : max(|gb|_1, |gc|_1)
+//   eo, ed : twice the abs error of b(o)/c(o) (+ 8u for the weights' own
+//            rounding) and of b(d)/c(d) (max of the two forms); the factor 2
+//            makes one bound cover alpha = 1 - b - c as well
+//   g      : 2 max(|gb|_1, |gc|_1)
 //   qhi    : |q| above qhi is certainly > 1e-5 (the reference's parallel test)
 //   grp    : coplanar group (host-verified in f64).  A line whose origin lies
 //            on a triangle of the same group meets this plane at |t| < 1e-4,
@@ -223,20 +224,27 @@ PT_HD RayPlane ray_plane(const UnitF& U, float h, F3 d, float hi_lo, float hi_hi
     return p;
 }
 
-// Barycentric part (per ray and triangle): kMiss when the reference certainly
-// reports no usable intersection, kCand when it certainly reports one (|t|
-// in [at - dt, at + dt]), kAmb otherwise.  Branch-free.
-PT_HD int classify_tri(const TriB& B, const RayPlane& p, float bo, float co, F3 d) {
+// Barycentric part (per ray and triangle), branch-free.  With
+// del = g dt + |t| ed + eo, the host constants already carry the factor 2:
+// |beta_ref - beta|, |gamma_ref - gamma| <= del/2 and |alpha_ref - alpha|
+// <= del (alpha = 1 - beta - gamma), so with m = min(beta, gamma, alpha):
+//   m < -del  -> some true weight < 0: certainly outside
+//   m >  del  -> every true weight > 0: certainly inside
+struct Verdict {
+    bool cand;   // the reference certainly reports a usable intersection
+    bool amb;    // undecided: evaluate in f64
+};
+PT_HD Verdict classify_tri(const TriB& B, const RayPlane& p, float bo, float co, F3 d) {
     const float beta = fmaf(p.t, lin3(B.gb, d), bo);
     const float gam = fmaf(p.t, lin3(B.gc, d), co);
-    const float alpha = (1.0f - beta) - gam;
-    // |beta_ref - beta| <= del, |gamma_ref - gamma| <= del,
-    // |alpha_ref - alpha| <= 2 del (eo carries the 8u rounding slack)
+    const float m = min3f(beta, gam, (1.0f - beta) - gam);
     const float del = fmaf(B.g, p.dt, fmaf(p.at, B.ed, B.eo));
-    const bool out = min3f(beta, gam, alpha + del) < -del;
-    const bool in = min3f(beta, gam, alpha - del) > del;
-    return (p.rmiss | out) ? kMiss : ((p.rcand & in) ? kCand : kAmb);
+    Verdict v;
+    v.cand = p.rcand & (m > del);
+    v.amb = !(p.rmiss | (m < -del)) & !v.cand;
+    return v;
 }
+PT_HD int verdict_code(Verdict v) { return v.cand ? kCand : (v.amb ? kAmb : kMiss); }
 
 // ------------------------------------------------------ light sampling --
 // pick_random_triangle, utils.py:28-39: first i with cum[i] <= n < cum[i+1]

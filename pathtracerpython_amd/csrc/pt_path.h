@@ -88,8 +88,7 @@ template <bool COUNT>
 PT_HD void closest_tri(const SceneK& S, const TriB& B, const RayPlane& p, float bo, float co,
                        F3 d32, bool coplanar, const Spill& sp, int o_slot, int dn_slot,
                        ClosestAcc* acc, Counters* cnt) {
-    int st = classify_tri(B, p, bo, co, d32);
-    if (coplanar) st = kMiss;
+    const int st = coplanar ? kMiss : verdict_code(classify_tri(B, p, bo, co, d32));
     float a = (st == kCand) ? p.at - p.dt : INFINITY;
     float b = (st == kCand) ? p.at + p.dt : INFINITY;
     if (st == kAmb) {   // rare: decide this test in f64
@@ -212,43 +211,6 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, u
     sh->leak = S.n_obj - 1;
 }
 
-template <bool FORCE64, bool COUNT>
-PT_HD void shadow_tri(const SceneK& S, const TriB& B, int k, int st, ShadowSet* sh,
-                      const Spill& sp, Counters* cnt) {
-    bool hit = (st == kCand);
-    if (st == kAmb && !sh->occ[k]) {   // rare (FORCE64: always) — f64 decision
-        D3 Q;
-        double sqd;
-        if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
-        const D3 P = sp.get3(kSpP), L = sp.get3(kSpL + 3 * k);
-        hit = eval64(S.trid[B.t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
-              sqd < squared_dist(P, L);
-    }
-    if (hit && !sh->occ[k]) {
-        sh->occ[k] = true;
-        sh->first[k] = B.t + 1;
-        if (k == kLightSamples - 1) sh->leak = S.tri_obj[B.t];
-    }
-}
-
-// The 3 shadow rays against one plane unit, triangles in scene order.
-template <bool FORCE64, bool COUNT>
-PT_HD void shadow_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
-                       ShadowSet* sh, const Spill& sp, Counters* cnt) {
-#pragma unroll
-    for (int k = 0; k < kLightSamples; ++k) {
-        int st0 = kAmb, st1 = kAmb;
-        if (!FORCE64) {
-            const RayPlane p = ray_plane(U, O.h, sh->d32[k], sh->hlo[k], sh->hhi[k]);
-            st0 = coplanar ? kMiss : classify_tri(U.tri[0], p, O.bo0, O.co0, sh->d32[k]);
-            if (U.count == 2)
-                st1 = coplanar ? kMiss : classify_tri(U.tri[1], p, O.bo1, O.co1, sh->d32[k]);
-        }
-        shadow_tri<FORCE64, COUNT>(S, U.tri[0], k, st0, sh, sp, cnt);
-        if (U.count == 2) shadow_tri<FORCE64, COUNT>(S, U.tri[1], k, st1, sh, sp, cnt);
-    }
-}
-
 // One plane unit against the 3 shadow rays and the next ray's closest hit,
 // all from the same origin (the fused per-bounce pass).  Every verdict is
 // computed branch-free; ambiguous tests are only recorded as bits and
@@ -270,31 +232,42 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
     if (do_shadow) {
 #pragma unroll
         for (int k = 0; k < kLightSamples; ++k) {
-            int st0 = kAmb, st1 = kAmb;
+            bool c0 = false, c1 = false, a0 = true, a1 = two;
             if (!FORCE64) {
                 const RayPlane p = ray_plane(U, O.h, sh->d32[k], sh->hlo[k], sh->hhi[k]);
-                st0 = coplanar ? kMiss : classify_tri(U.tri[0], p, O.bo0, O.co0, sh->d32[k]);
-                st1 = (coplanar || !two) ? kMiss : classify_tri(U.tri[1], p, O.bo1, O.co1, sh->d32[k]);
-            } else if (!two) {
-                st1 = kMiss;
+                const Verdict v0 = classify_tri(U.tri[0], p, O.bo0, O.co0, sh->d32[k]);
+                c0 = v0.cand & !coplanar;
+                a0 = v0.amb & !coplanar;
+                a1 = false;
+                if (two) {   // wave-uniform
+                    const Verdict v1 = classify_tri(U.tri[1], p, O.bo1, O.co1, sh->d32[k]);
+                    c1 = v1.cand & !coplanar;
+                    a1 = v1.amb & !coplanar;
+                }
             }
-            const bool c0 = (st0 == kCand), c1 = (st1 == kCand);
-            if (COUNT && !occ0[k] && (c0 || c1)) sh->first[k] = (c0 ? U.tri[0].t : U.tri[1].t) + 1;
-            if (k == kLightSamples - 1 && !occ0[k] && (c0 || c1)) sh->leak = S.tri_obj[U.tri[0].t];
-            sh->occ[k] = occ0[k] || c0 || c1;
-            if (!occ0[k]) amb |= ((st0 == kAmb) ? 1u : 0u) << (2 * k) | ((st1 == kAmb) ? 2u : 0u) << (2 * k);
+            const bool newly = !occ0[k] & (c0 | c1);
+            if (COUNT && newly) sh->first[k] = (c0 ? U.tri[0].t : U.tri[1].t) + 1;
+            if (k == kLightSamples - 1 && newly) sh->leak = S.tri_obj[U.tri[0].t];
+            sh->occ[k] = occ0[k] | c0 | c1;
+            if (!occ0[k]) amb |= (a0 ? 1u : 0u) << (2 * k) | (a1 ? 2u : 0u) << (2 * k);
         }
     }
     if (!FORCE64 && do_closest) {
         const RayPlane p = ray_plane(U, O.h, n32, INFINITY, INFINITY);
-        int st0 = coplanar ? kMiss : classify_tri(U.tri[0], p, O.bo0, O.co0, n32);
-        int st1 = (coplanar || !two) ? kMiss : classify_tri(U.tri[1], p, O.bo1, O.co1, n32);
+        const Verdict v0 = classify_tri(U.tri[0], p, O.bo0, O.co0, n32);
+        bool c0 = v0.cand & !coplanar, c1 = false, a1 = false;
+        const bool a0 = v0.amb & !coplanar;
+        if (two) {
+            const Verdict v1 = classify_tri(U.tri[1], p, O.bo1, O.co1, n32);
+            c1 = v1.cand & !coplanar;
+            a1 = v1.amb & !coplanar;
+        }
         // both candidates of one unit cannot happen (a point certainly inside
         // one triangle is certainly outside its coplanar neighbour)
-        const bool c = (st0 == kCand) || (st1 == kCand);
-        closest_add(ca, (st0 == kCand) ? U.tri[0].t : U.tri[1].t, c ? p.at - p.dt : INFINITY,
+        const bool c = c0 | c1;
+        closest_add(ca, c0 ? U.tri[0].t : U.tri[1].t, c ? p.at - p.dt : INFINITY,
                     c ? p.at + p.dt : INFINITY);
-        amb |= ((st0 == kAmb) ? 64u : 0u) | ((st1 == kAmb) ? 128u : 0u);
+        amb |= (a0 ? 64u : 0u) | (a1 ? 128u : 0u);
     }
     if (amb) {   // rare (FORCE64: every shadow test) — decide in f64
         const D3 P = sp.get3(kSpP);
@@ -362,7 +335,8 @@ PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
         if (PT_WAVE_ALL(sh.occ[0] && sh.occ[1] && sh.occ[2])) break;
         const UnitF U = S.unit[u];
         const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
-        shadow_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, &sh, sp, cnt);
+        fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, true, false, &sh, F3{0.f, 0.f, 0.f},
+                                   nullptr, sp, cnt);
     }
     return shadow_color<COUNT>(S, n, obj, sh, sp, cnt);
 }

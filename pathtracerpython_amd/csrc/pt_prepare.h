@@ -139,9 +139,10 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         P.eh = s * 8 * u * (n1 * X + fabs(chn));
         // q's own error, plus 8u n1 >= 8u|q| covering the rounding of 1/q and t
         P.eq = s * 8 * u * n1 + 8 * u * n1;
-        B.eo = f32_up(s * 8 * u * std::max(gb1 * X + fabs(cb), gc1 * X + fabs(cc)) + 8 * u);
-        B.ed = f32_up(s * 8 * u * std::max(gb1, gc1));
-        B.g = f32_up(std::max(gb1, gc1) * (1 + 1e-3));
+        // x2: one bound for beta, gamma (error <= del/2) and alpha (<= del)
+        B.eo = f32_up(2 * (s * 8 * u * std::max(gb1 * X + fabs(cb), gc1 * X + fabs(cc)) + 8 * u));
+        B.ed = f32_up(2 * s * 8 * u * std::max(gb1, gc1));
+        B.g = f32_up(2 * std::max(gb1, gc1) * (1 + 1e-3));
     }
     // coplanar groups: triangle t joins the group of an earlier
     // representative r when every vertex of t lies within 1e-12 of r's plane
@@ -214,8 +215,8 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
                 if (pair) {
                     eh = std::max(eh, pl[t + 1].eh) + 1e-9;
                     eq = std::max(eq, pl[t + 1].eq) + 1e-9;
-                    U.tri[0].eo = f32_up(U.tri[0].eo + 1e-9);
-                    U.tri[1].eo = f32_up(U.tri[1].eo + 1e-9);
+                    U.tri[0].eo = f32_up(U.tri[0].eo + 2e-9);
+                    U.tri[1].eo = f32_up(U.tri[1].eo + 2e-9);
                 }
                 for (int i = 0; i < 3; ++i) U.n[i] = (float)P.n[i];
                 U.cn = (float)P.cn;

@@ -111,7 +111,7 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
                 D3 Q; double sqd;
                 const bool h = eval64(H.trid[B.t], o, dn, &Q, &sqd);
                 // closest semantics
-                int st = classify_tri(B, pc, bo, co, d32);
+                int st = verdict_code(classify_tri(B, pc, bo, co, d32));
                 const bool ref_c = h && sqd > kZero;
                 ++tests;
                 if (st == kAmb) ++amb;
@@ -122,7 +122,7 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
                     if (sq < (double)pc.at - pc.dt || sq > (double)pc.at + pc.dt) ++wrong;
                 }
                 // shadow semantics
-                st = classify_tri(B, ps, bo, co, d32);
+                st = verdict_code(classify_tri(B, ps, bo, co, d32));
                 const bool ref_s = h && !(sqd < kZero) && sqd < lim;
                 ++tests;
                 if (st == kAmb) ++amb;
