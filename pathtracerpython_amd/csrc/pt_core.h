@@ -208,6 +208,7 @@ enum : int { kMiss = 0, kCand = 1, kAmb = 2 };
 //   shadow : occluder iff 1e-5 <= sqd < |L - P|^2 -> hi_lo/hi_hi bracket tL
 struct RayPlane {
     float t, at, dt;
+    float del;     // barycentric bound, shared by the unit's triangles (see classify_tri)
     bool rmiss;    // |t| certainly out of range: the test is a certain miss
     bool rcand;    // |t| certainly in range and |q| certainly > 1e-5
 };
@@ -219,13 +220,16 @@ PT_HD RayPlane ray_plane(const UnitF& U, float h, F3 d, float hi_lo, float hi_hi
     p.at = fabsf(p.t);
     // |t_ref - t| <= (eh + |t| eq) / |q|  (eq absorbs the 3u|t| of 1/q and t)
     p.dt = fabsf(r) * fmaf(p.at, U.eq, U.eh);
+    // the host stores the unit's bound coefficients (max over its triangles)
+    // in every member's eo/ed/g, so one del serves both triangles
+    p.del = fmaf(U.tri[0].g, p.dt, fmaf(p.at, U.tri[0].ed, U.tri[0].eo));
     p.rmiss = (p.at + p.dt < kTzLo) | (p.at - p.dt >= hi_hi);
     p.rcand = (fabsf(q) > U.qhi) & (p.at - p.dt > kTzHi) & (p.at + p.dt < hi_lo);
     return p;
 }
 
 // Barycentric part (per ray and triangle), branch-free.  With
-// del = g dt + |t| ed + eo, the host constants already carry the factor 2:
+// del = g dt + |t| ed + eo (unit-wide coefficients), the host constants already carry the factor 2:
 // |beta_ref - beta|, |gamma_ref - gamma| <= del/2 and |alpha_ref - alpha|
 // <= del (alpha = 1 - beta - gamma), so with m = min(beta, gamma, alpha):
 //   m < -del  -> some true weight < 0: certainly outside
@@ -238,7 +242,7 @@ PT_HD Verdict classify_tri(const TriB& B, const RayPlane& p, float bo, float co,
     const float beta = fmaf(p.t, lin3(B.gb, d), bo);
     const float gam = fmaf(p.t, lin3(B.gc, d), co);
     const float m = min3f(beta, gam, (1.0f - beta) - gam);
-    const float del = fmaf(B.g, p.dt, fmaf(p.at, B.ed, B.eo));
+    const float del = p.del;
     Verdict v;
     v.cand = p.rcand & (m > del);
     v.amb = !(p.rmiss | (m < -del)) & !v.cand;

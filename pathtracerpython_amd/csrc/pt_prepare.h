@@ -215,8 +215,12 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
                 if (pair) {
                     eh = std::max(eh, pl[t + 1].eh) + 1e-9;
                     eq = std::max(eq, pl[t + 1].eq) + 1e-9;
-                    U.tri[0].eo = f32_up(U.tri[0].eo + 2e-9);
-                    U.tri[1].eo = f32_up(U.tri[1].eo + 2e-9);
+                    // one bound for both members (the kernel evaluates del once per
+                    // ray and unit from tri[0]'s coefficients)
+                    const float eo = f32_up(std::max(U.tri[0].eo, U.tri[1].eo) + 2e-9);
+                    const float ed = std::max(U.tri[0].ed, U.tri[1].ed);
+                    const float g = std::max(U.tri[0].g, U.tri[1].g);
+                    for (TriB& B : U.tri) { B.eo = eo; B.ed = ed; B.g = g; }
                 }
                 for (int i = 0; i < 3; ++i) U.n[i] = (float)P.n[i];
                 U.cn = (float)P.cn;
