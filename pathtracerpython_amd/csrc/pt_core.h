@@ -68,7 +68,7 @@ struct alignas(16) UnitF {   // 144 B: two s_load_dwordx16 + one dwordx4
     float n[3], cn;
     float eh, eq, qhi;
     int32_t grp;
-    int32_t count, pad0, pad1, pad2;
+    int32_t count, obj, pad1, pad2;   // obj: the members' object (one per unit)
     TriB tri[2];
 };
 

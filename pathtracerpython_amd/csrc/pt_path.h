@@ -247,7 +247,7 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
             }
             const bool newly = !occ0[k] & (c0 | c1);
             if (COUNT && newly) sh->first[k] = (c0 ? U.tri[0].t : U.tri[1].t) + 1;
-            if (k == kLightSamples - 1 && newly) sh->leak = S.tri_obj[U.tri[0].t];
+            if (k == kLightSamples - 1 && newly) sh->leak = U.obj;
             sh->occ[k] = occ0[k] | c0 | c1;
             if (!occ0[k]) amb |= (a0 ? 1u : 0u) << (2 * k) | (a1 ? 2u : 0u) << (2 * k);
         }

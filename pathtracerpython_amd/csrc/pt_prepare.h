@@ -204,6 +204,7 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
                               d->tri_obj[t + 1] == d->tri_obj[t];
             U.count = pair ? 2 : 1;
             U.grp = H->tri_grp[t];
+            U.obj = d->tri_obj[t];
             U.tri[0] = tb[t];
             U.tri[1] = pair ? tb[t + 1] : TriB{};
             if (!P.ok) {   // degenerate: dt = -inf -> certain miss, never a candidate
