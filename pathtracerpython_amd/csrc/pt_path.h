@@ -466,7 +466,8 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
                                     &ca, cnt);
             }
         }
-        const D3 col = shadow_color<COUNT>(S, ld3(R.n), obj, sh, sp, cnt);
+        // the normal is re-read rather than kept live across the unit loop
+        const D3 col = shadow_color<COUNT>(S, ld3(S.tris[tri].n), obj, sh, sp, cnt);
         acc = acc + col * k;   // main.py:230-231 (k before this bounce's update)
         k = kk;
         bool done = !trace;
