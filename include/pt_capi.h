@@ -147,6 +147,20 @@ int pt_compute_color(pt_scene* scene, const int32_t* obj, const double* point,
                      const double* normal, const double* u, int64_t n,
                      double* out_rgb);
 
+/* Image finalisation of make_image (utils.py:150-161) on the device:
+ * global min over the whole height x width x 3 array, shift, divide by the
+ * shifted maximum, x255, truncate to uint8 — in f64, as numpy does (a NaN
+ * anywhere, or a constant image, gives 0s like numpy's cast on x86).
+ * fb: a full framebuffer as pt_render* writes it (image orientation, f32, or
+ * f64 with PT_FLAG_OUT_F64 in flags); out: height*width*3 uint8 in the same
+ * layout, which is make_image's array for the square images the reference
+ * supports (for width != height its placement, utils.py:154-156, indexes out
+ * of range).  The _device form is asynchronous on `stream`. */
+int pt_image_u8_device(const void* fb_dev, int32_t width, int32_t height, uint32_t flags,
+                       void* out_u8_dev, void* stream);
+int pt_image_u8(const void* fb_host, int32_t width, int32_t height, uint32_t flags,
+                uint8_t* out_u8_host);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,6 +35,8 @@ def _bind(lib):
         "pt_last_kernel_ms": ([vp, C.POINTER(C.c_float)], C.c_int),
         "pt_intersect_objects": ([vp, dp, C.c_int64, ip, dp], C.c_int),
         "pt_compute_color": ([vp, ip, dp, dp, dp, C.c_int64, dp], C.c_int),
+        "pt_image_u8_device": ([vp, C.c_int32, C.c_int32, C.c_uint32, vp, vp], C.c_int),
+        "pt_image_u8": ([vp, C.c_int32, C.c_int32, C.c_uint32, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -45,7 +47,8 @@ def _bind(lib):
 
 EXPORTS = ("pt_api_version", "pt_last_error", "pt_device_count", "pt_scene_create",
            "pt_scene_destroy", "pt_band_rows", "pt_render_device", "pt_render",
-           "pt_last_kernel_ms", "pt_intersect_objects", "pt_compute_color")
+           "pt_last_kernel_ms", "pt_intersect_objects", "pt_compute_color",
+           "pt_image_u8_device", "pt_image_u8")
 
 
 def lib():

@@ -17,6 +17,7 @@
 
 #include "pt_path.h"
 #include "pt_prepare.h"
+#include "pt_image.h"
 
 using namespace pt;
 
@@ -416,6 +417,59 @@ int pt_last_kernel_ms(pt_scene* s, float* ms) {
     HIPCHK(hipEventSynchronize(s->ev1));
     HIPCHK(hipEventElapsedTime(ms, s->ev0, s->ev1));
     return PT_OK;
+}
+
+int pt_image_u8_device(const void* fb_dev, int32_t width, int32_t height, uint32_t flags,
+                       void* out_u8_dev, void* stream) {
+    if (!fb_dev || !out_u8_dev) return fail(PT_EINVAL, "null buffer");
+    if (width <= 0 || height <= 0) return fail(PT_EINVAL, "need width, height > 0");
+    const int64_t n = (int64_t)width * height * 3;
+    hipStream_t st = (hipStream_t)stream;
+    unsigned long long* keys = nullptr;
+    HIPCHK(hipMallocAsync((void**)&keys, 2 * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(keys, 0xff, sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(keys + 1, 0, sizeof(unsigned long long), st));
+    // 4 elements per thread step when the buffers allow 16-byte loads and
+    // 4-byte stores; ~8 blocks per CU of grid-stride work
+    const int vec = ((uintptr_t)fb_dev % 16 == 0) && ((uintptr_t)out_u8_dev % 4 == 0);
+    const int blocks = (int)std::min<int64_t>((n / 4 + 255) / 256 + 1, 2048);
+    if (flags & PT_FLAG_OUT_F64) {
+        hipLaunchKernelGGL(k_minmax<double>, dim3(blocks), dim3(256), 0, st, (const double*)fb_dev, n, vec, keys);
+        hipLaunchKernelGGL(k_to_u8<double>, dim3(blocks), dim3(256), 0, st, (const double*)fb_dev, n, vec, keys,
+                           (uint8_t*)out_u8_dev);
+    } else {
+        hipLaunchKernelGGL(k_minmax<float>, dim3(blocks), dim3(256), 0, st, (const float*)fb_dev, n, vec, keys);
+        hipLaunchKernelGGL(k_to_u8<float>, dim3(blocks), dim3(256), 0, st, (const float*)fb_dev, n, vec, keys,
+                           (uint8_t*)out_u8_dev);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipFreeAsync(keys, st));
+    return PT_OK;
+}
+
+int pt_image_u8(const void* fb_host, int32_t width, int32_t height, uint32_t flags,
+                uint8_t* out_u8_host) {
+    if (!fb_host || !out_u8_host) return fail(PT_EINVAL, "null buffer");
+    if (width <= 0 || height <= 0) return fail(PT_EINVAL, "need width, height > 0");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(PT_ENODEV, "no HIP device");
+    const size_t n = (size_t)width * height * 3;
+    const size_t in_bytes = n * ((flags & PT_FLAG_OUT_F64) ? sizeof(double) : sizeof(float));
+    void *d_in = nullptr, *d_out = nullptr;
+    HIPCHK(hipMalloc(&d_in, in_bytes));
+    if (hipMalloc(&d_out, n) != hipSuccess) {
+        (void)hipFree(d_in);
+        return fail(PT_ENOMEM, "hipMalloc failed");
+    }
+    int rc = PT_OK;
+    if (hipMemcpy(d_in, fb_host, in_bytes, hipMemcpyHostToDevice) != hipSuccess)
+        rc = fail(PT_EHIP, "hipMemcpy to device failed");
+    if (!rc) rc = pt_image_u8_device(d_in, width, height, flags, d_out, nullptr);
+    if (!rc && hipMemcpy(out_u8_host, d_out, n, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(PT_EHIP, "hipMemcpy to host failed");
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return rc;
 }
 
 int pt_intersect_objects(pt_scene* s, const double* rays, int64_t n, int32_t* out_tri,

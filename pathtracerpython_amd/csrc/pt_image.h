@@ -1,0 +1,128 @@
+// pt_image.h — image finalisation of the reference's make_image
+// (utils.py:150-161) on the device: global min over the whole H x W x 3
+// array, shift, divide by the shifted maximum, x255, truncation to uint8.
+//
+// Two passes over the framebuffer (HBM-bound: 2 reads of 12 B (f32) or
+// 24 B (f64) per pixel + a 3 B write):
+//   k_minmax  grid-stride reduction; each block folds its min/max into two
+//             64-bit keys with one atomicMin/atomicMax (an order-preserving
+//             map of the doubles, so the result is exact and independent of
+//             the order blocks finish in);
+//   k_to_u8   elementwise ((x - min) / (max - min)) * 255 -> uint8, in f64
+//             as numpy does.
+// numpy semantics kept: a NaN anywhere makes every output NaN, which
+// astype('uint8') turns into 0 on x86; a constant image (max - min == 0)
+// gives 0/0 = NaN -> 0 as well.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pt {
+
+// order-preserving double -> uint64 (for atomicMin/atomicMax on the bits)
+__device__ __forceinline__ uint64_t order_key(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double key_value(uint64_t k) {
+    const uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    return __longlong_as_double((long long)b);
+}
+
+template <typename T>
+__device__ __forceinline__ double load_f64(const T* p, int64_t i) { return (double)p[i]; }
+
+// 4 consecutive elements as doubles (one 16-byte load for f32, two for f64);
+// the caller guarantees 16-byte alignment of p + 4i
+__device__ __forceinline__ void load4(const float* p, int64_t i, double v[4]) {
+    const float4 f = reinterpret_cast<const float4*>(p)[i];
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+}
+__device__ __forceinline__ void load4(const double* p, int64_t i, double v[4]) {
+    const double2 a = reinterpret_cast<const double2*>(p)[2 * i];
+    const double2 b = reinterpret_cast<const double2*>(p)[2 * i + 1];
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+}
+
+// keys[0] = min key (init ~0), keys[1] = max key (init 0).  Vector body over
+// n4 = n/4 groups when `vec` (16-byte aligned input), scalar tail.
+template <typename T>
+__global__ __launch_bounds__(256) void k_minmax(const T* __restrict__ fb, int64_t n, int vec,
+                                                unsigned long long* __restrict__ keys) {
+    uint64_t kmin = ~0ull, kmax = 0ull;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n4 = vec ? n / 4 : 0;
+    for (int64_t i = gid; i < n4; i += stride) {
+        double v[4];
+        load4(fb, i, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t k = order_key(v[j]);
+            kmin = k < kmin ? k : kmin;
+            kmax = k > kmax ? k : kmax;
+        }
+    }
+    for (int64_t i = 4 * n4 + gid; i < n; i += stride) {
+        const uint64_t k = order_key(load_f64(fb, i));
+        kmin = k < kmin ? k : kmin;
+        kmax = k > kmax ? k : kmax;
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t a = (uint64_t)__shfl_xor((unsigned long long)kmin, m);
+        const uint64_t b = (uint64_t)__shfl_xor((unsigned long long)kmax, m);
+        kmin = a < kmin ? a : kmin;
+        kmax = b > kmax ? b : kmax;
+    }
+    __shared__ uint64_t smin[4], smax[4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { smin[w] = kmin; smax[w] = kmax; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int j = 1; j < 4; ++j) {
+            kmin = smin[j] < kmin ? smin[j] : kmin;
+            kmax = smax[j] > kmax ? smax[j] : kmax;
+        }
+        atomicMin(&keys[0], (unsigned long long)kmin);
+        atomicMax(&keys[1], (unsigned long long)kmax);
+    }
+}
+
+// NaN keys sit above +inf (positive NaN) or below -inf (negative NaN)
+__device__ __forceinline__ bool key_is_nan(uint64_t k) {
+    return k > 0xfff0000000000000ull || k < 0x000fffffffffffffull;
+}
+
+__device__ __forceinline__ uint32_t to_u8(double x, double mn, double mx, bool nan) {
+    const double v = ((x - mn) / mx) * 255.0;
+    // astype('uint8'): truncation; NaN (constant image 0/0, or a NaN input)
+    // -> 0 as x86's conversion gives
+    return (nan || !(v == v)) ? 0u : (uint32_t)(int)v;
+}
+
+// `vec`: input 16-byte and output 4-byte aligned -> 4 elements per step,
+// one packed 32-bit store
+template <typename T>
+__global__ __launch_bounds__(256) void k_to_u8(const T* __restrict__ fb, int64_t n, int vec,
+                                               const unsigned long long* __restrict__ keys,
+                                               uint8_t* __restrict__ out) {
+    const uint64_t kmin = keys[0], kmax = keys[1];
+    const bool nan = key_is_nan(kmin) || key_is_nan(kmax);
+    const double mn = key_value(kmin);
+    const double mx = key_value(kmax) - mn;   // np.max(mat - min) = fl(max - min)
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n4 = vec ? n / 4 : 0;
+    for (int64_t i = gid; i < n4; i += stride) {
+        double v[4];
+        load4(fb, i, v);
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w |= to_u8(v[j], mn, mx, nan) << (8 * j);
+        reinterpret_cast<uint32_t*>(out)[i] = w;
+    }
+    for (int64_t i = 4 * n4 + gid; i < n; i += stride)
+        out[i] = (uint8_t)to_u8(load_f64(fb, i), mn, mx, nan);
+}
+
+}  // namespace pt

@@ -245,7 +245,7 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
                     a1 = v1.amb & !coplanar;
                 }
             }
-            const bool newly = !occ0[k] & (c0 | c1);
+            const bool newly = (!occ0[k]) & (c0 | c1);
             if (COUNT && newly) sh->first[k] = (c0 ? U.tri[0].t : U.tri[1].t) + 1;
             if (k == kLightSamples - 1 && newly) sh->leak = U.obj;
             sh->occ[k] = occ0[k] | c0 | c1;

@@ -49,12 +49,22 @@ def main(argv=None):
         print('note: the 3-D scene viewer (plot.py) is not part of this build; ignoring --show-*',
               file=sys.stderr)
     with Renderer(scene) as r:
-        fb = r.render(W, H, spp=args.n_rays, bounces=args.n_bounces, seed=args.seed, rr=args.rr)
+        if W == H:   # make_image on the device (utils.py:150-161)
+            arr, fb = r.render_image(W, H, spp=args.n_rays, bounces=args.n_bounces,
+                                     seed=args.seed, rr=args.rr, return_fb=True)
+        else:        # the reference's placement for W != H (utils.py:154-156), on the host
+            fb = r.render(W, H, spp=args.n_rays, bounces=args.n_bounces, seed=args.seed,
+                          rr=args.rr)
+            arr = None
         print(f'render: {W}x{H}, {args.n_rays} spp, {args.n_bounces} bounces, '
               f'kernel {r.last_kernel_ms():.3f} ms')
     if args.save_raw:
         np.save(args.save_raw, fb)
-    im = framebuffer_to_image(fb)
+    if arr is not None:
+        from PIL import Image
+        im = Image.fromarray(arr)
+    else:
+        im = framebuffer_to_image(fb)
     if args.out is not None:
         im.save(args.out)
     if args.show_img:

@@ -79,6 +79,23 @@ class Renderer:
                                                  C.c_void_p(stream or 0), None),
                       "pt_render_device")
 
+    def render_image(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
+                     rr_depth=3, return_fb=False):
+        """make_image's uint8 array (H, W, 3) of a full render, finalised on
+        the device (pt_image_u8_device) from the float64 framebuffer; with
+        return_fb also that framebuffer.  Square images are exactly what
+        make_image (utils.py:150-161) returns for the same colours."""
+        import torch
+        p = self.params(width, height, spp, bounces, seed, rr, rr_depth, out_f64=True)
+        W, H = p.width, p.height
+        fb = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
+        img = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        self.render_device(p, fb.data_ptr(), s)
+        image_u8_device(fb.data_ptr(), W, H, True, img.data_ptr(), s)
+        img = img.cpu().numpy()
+        return (img, fb.cpu().numpy()) if return_fb else img
+
     def last_kernel_ms(self):
         ms = C.c_float(0)
         _native.check(self._lib.pt_last_kernel_ms(self._h, C.byref(ms)), "pt_last_kernel_ms")
@@ -140,6 +157,31 @@ def render(scene, width=None, height=None, spp=1, bounces=1, seed=None, rr=False
     """main.py's render as a function: framebuffer (H, W, 3) float32."""
     with Renderer(scene) as r:
         return r.render(width, height, spp, bounces, seed, rr, rr_depth)
+
+
+def image_u8_device(fb_ptr, width, height, f64, out_ptr, stream=None):
+    """Device image finalisation (make_image, utils.py:150-161) of a full
+    framebuffer at fb_ptr (f32, or f64) into height*width*3 uint8 at out_ptr,
+    asynchronous on a HIP stream handle."""
+    lib = _native.lib()
+    _native.check(lib.pt_image_u8_device(C.c_void_p(fb_ptr), int(width), int(height),
+                                         PT_FLAG_OUT_F64 if f64 else 0, C.c_void_p(out_ptr),
+                                         C.c_void_p(stream or 0)), "pt_image_u8_device")
+
+
+def image_u8(fb):
+    """make_image's normalisation of a host framebuffer (H, W, 3) float32 or
+    float64, computed on the GPU: global min-max, x255, uint8 truncation."""
+    fb = np.asarray(fb)
+    if fb.dtype not in (np.float32, np.float64):
+        fb = fb.astype(np.float64)
+    fb = np.ascontiguousarray(fb)
+    H, W = fb.shape[:2]
+    out = np.zeros((H, W, 3), dtype=np.uint8)
+    _native.check(_native.lib().pt_image_u8(C.c_void_p(fb.ctypes.data), W, H,
+                                            PT_FLAG_OUT_F64 if fb.dtype == np.float64 else 0,
+                                            C.c_void_p(out.ctypes.data)), "pt_image_u8")
+    return out
 
 
 def to_list_order(fb):

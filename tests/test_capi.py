@@ -102,3 +102,12 @@ def test_list_order_roundtrip():
         ix, iy = divmod(k, H)
         assert np.array_equal(fb[H - 1 - iy, ix], cols[k])
     assert np.array_equal(to_list_order(fb), cols)
+
+
+def test_image_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from pathtracerpython_amd.render import image_u8
+    with pytest.raises(_native.NativeError, match="no HIP device"):
+        image_u8(np.zeros((2, 2, 3)))

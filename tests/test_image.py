@@ -1,0 +1,67 @@
+"""Device image finalisation (pt_image_u8*) against
+the reference's make_image (utils.py:150-161): bit-exact uint8.  The golden
+PNG arrays were produced by the reference itself (tests/golden/gen_golden.py);
+other cases compare with the numpy restatement utils.normalize_to_uint8,
+which is the reference's own four lines."""
+import warnings
+
+import numpy as np
+import pytest
+
+from conftest import golden_renders
+from pathtracerpython_amd.render import Renderer, image_u8
+from pathtracerpython_amd.utils import normalize_to_uint8
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def R(cornell):
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    r = Renderer(cornell)
+    yield r
+    r.close()
+
+
+def _numpy_u8(a):
+    with warnings.catch_warnings(), np.errstate(all="ignore"):
+        warnings.simplefilter("ignore")
+        return normalize_to_uint8(a)
+
+
+@pytest.mark.parametrize("name,g", golden_renders(), ids=[n for n, _ in golden_renders()])
+def test_device_image_matches_reference_png(R, name, g):
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    img, fb = R.render_image(W, H, spp, B, seed, return_fb=True)
+    assert img.dtype == np.uint8 and img.shape == (H, W, 3)
+    assert np.array_equal(img, g["png"]), name
+    assert np.array_equal(image_u8(fb), g["png"])
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("shape", [(1, 1), (7, 3), (64, 64), (509, 1031)])
+def test_image_u8_matches_numpy(dtype, shape):
+    rs = np.random.RandomState(sum(shape))
+    a = (rs.normal(0.2, 0.7, shape + (3,)) ** 3).astype(dtype)   # negatives, wide range
+    assert np.array_equal(image_u8(a), _numpy_u8(a))
+
+
+def test_image_u8_edge_cases():
+    const = np.full((8, 8, 3), 0.25)
+    assert np.array_equal(image_u8(const), _numpy_u8(const))   # 0/0 -> 0
+    a = np.linspace(-1, 1, 8 * 8 * 3).reshape(8, 8, 3)
+    a[3, 4, 1] = np.nan
+    assert np.array_equal(image_u8(a), _numpy_u8(a))           # NaN poisons min/max
+    b = np.linspace(-1, 1, 8 * 8 * 3).reshape(8, 8, 3)
+    b[0, 0, 0] = np.inf
+    assert np.array_equal(image_u8(b), _numpy_u8(b))
+    c = np.zeros((4, 4, 3))
+    c[1, 1, 1] = 1e-300                                        # denormal-scale range
+    assert np.array_equal(image_u8(c), _numpy_u8(c))
+
+
+def test_image_u8_large_f32():
+    rs = np.random.RandomState(5)
+    a = rs.uniform(-3, 7, (2048, 2048, 3)).astype(np.float32)
+    assert np.array_equal(image_u8(a), _numpy_u8(a))
