@@ -36,6 +36,7 @@ extern "C" {
 #define PT_EHIP (-2)       /* HIP runtime error */
 #define PT_ENOMEM (-3)     /* device or host allocation failed */
 #define PT_ENODEV (-4)     /* no usable gfx950 device */
+#define PT_EUNSUPPORTED (-5) /* pt_obj_load: input outside the fast reader's subset */
 
 /* pt_render flags */
 #define PT_FLAG_RR (1u << 0)           /* Russian roulette (build extension) */
@@ -160,6 +161,31 @@ int pt_image_u8_device(const void* fb_dev, int32_t width, int32_t height, uint32
                        void* out_u8_dev, void* stream);
 int pt_image_u8(const void* fb_host, int32_t width, int32_t height, uint32_t flags,
                 uint8_t* out_u8_host);
+
+/* Native OBJ reader (host only, no GPU needed) with the semantics of the
+ * reference's Obj (scene_reader.py:49-104, vector.py:143-173): comment and
+ * token rules, `v` / `f` records, negative indices, fan triangulation, and
+ * the per-triangle normal and area computed in the reference's operation
+ * order (bit-identical doubles).  Other commands are skipped; their raw line
+ * byte ranges are returned so a caller can report them as the reference
+ * prints them.  Returns PT_EUNSUPPORTED for inputs it does not mirror byte
+ * for byte (e.g. "1/2/3" face tokens, hex or underscore numbers, vertices
+ * with other than 3 coordinates, out-of-range indices, a zero-area
+ * triangle): the caller then falls back to the Python reader, which raises
+ * what the reference raises.  The mesh is owned by the library until
+ * pt_mesh_free. */
+typedef struct pt_mesh {
+    int64_t n_vert, n_tri, n_skip;
+    const double* vert;       /* [n_vert][3] */
+    const int64_t* face;      /* [n_tri][3] vertex indices as Obj.faces holds them */
+    const double* tri_v;      /* [n_tri][3][3] */
+    const double* tri_n;      /* [n_tri][3] */
+    const double* tri_area;   /* [n_tri] */
+    const int64_t* skip_off;  /* [n_skip] byte offset of each skipped line */
+    const int64_t* skip_len;  /* [n_skip] its length */
+} pt_mesh;
+int pt_obj_load(const char* path, pt_mesh** out);
+void pt_mesh_free(pt_mesh* mesh);
 
 #ifdef __cplusplus
 }

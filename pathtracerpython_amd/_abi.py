@@ -40,6 +40,15 @@ class PtRenderParams(C.Structure):
     ]
 
 
+class PtMesh(C.Structure):
+    """pt_mesh (include/pt_capi.h): a mesh read by pt_obj_load."""
+    _fields_ = [("n_vert", C.c_int64), ("n_tri", C.c_int64), ("n_skip", C.c_int64),
+                ("vert", C.POINTER(C.c_double)), ("face", C.POINTER(C.c_int64)),
+                ("tri_v", C.POINTER(C.c_double)), ("tri_n", C.POINTER(C.c_double)),
+                ("tri_area", C.POINTER(C.c_double)), ("skip_off", C.POINTER(C.c_int64)),
+                ("skip_len", C.POINTER(C.c_int64))]
+
+
 class PtStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "closest_tests", "shadow_tests", "ray_bounces", "shading_points",

@@ -18,6 +18,7 @@
 #include "pt_path.h"
 #include "pt_prepare.h"
 #include "pt_image.h"
+#include "pt_ingest.h"
 
 using namespace pt;
 
@@ -470,6 +471,49 @@ int pt_image_u8(const void* fb_host, int32_t width, int32_t height, uint32_t fla
     (void)hipFree(d_in);
     (void)hipFree(d_out);
     return rc;
+}
+
+struct pt_mesh_impl {
+    pt_mesh pub;
+    MeshOut data;
+};
+
+int pt_obj_load(const char* path, pt_mesh** out) {
+    if (!path || !out) return fail(PT_EINVAL, "null argument");
+    *out = nullptr;
+    pt_mesh_impl* m = new (std::nothrow) pt_mesh_impl();
+    if (!m) return fail(PT_ENOMEM, "out of host memory");
+    int rc;
+    try {
+        rc = parse_obj_file(path, &m->data);
+    } catch (const std::bad_alloc&) {
+        delete m;
+        return fail(PT_ENOMEM, "out of host memory");
+    }
+    if (rc != kIngestOk) {
+        delete m;
+        if (rc == kIngestIo) return fail(PT_EINVAL, std::string("cannot read ") + path);
+        return fail(PT_EUNSUPPORTED, rc == kIngestDivZero
+                                         ? "zero-area triangle (the reference divides by zero)"
+                                         : "input outside the fast reader's subset");
+    }
+    const MeshOut& d = m->data;
+    m->pub.n_vert = (int64_t)(d.vert.size() / 3);
+    m->pub.n_tri = (int64_t)d.tri_area.size();
+    m->pub.n_skip = (int64_t)d.skip_off.size();
+    m->pub.vert = d.vert.data();
+    m->pub.face = d.face.data();
+    m->pub.tri_v = d.tri_v.data();
+    m->pub.tri_n = d.tri_n.data();
+    m->pub.tri_area = d.tri_area.data();
+    m->pub.skip_off = d.skip_off.data();
+    m->pub.skip_len = d.skip_len.data();
+    *out = &m->pub;
+    return PT_OK;
+}
+
+void pt_mesh_free(pt_mesh* m) {
+    delete reinterpret_cast<pt_mesh_impl*>(m);   // pub is the first member
 }
 
 int pt_intersect_objects(pt_scene* s, const double* rays, int64_t n, int32_t* out_tri,

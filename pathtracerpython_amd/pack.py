@@ -14,35 +14,37 @@ from ._abi import PtSceneDesc
 MAT_KEYS = ('red', 'green', 'blue', 'ka', 'kd', 'ks', 'kt', 'n')
 
 
+def _mesh_arrays(g):
+    """(tri_v (n,3,3), tri_n (n,3), area (n,)) float64 of an Obj: the native
+    reader's arrays as they are, else built from the reference's lists."""
+    a = getattr(g, 'arrays', None)
+    if a is not None:
+        return a['tri_v'], a['tri_n'], a['tri_area']
+    n = len(g.triangles)
+    tv = np.array([[v[:3] for v in t] for t in g.triangles], dtype=np.float64).reshape(n, 3, 3)
+    tn = np.array([nv[:3] for nv in g.normals], dtype=np.float64).reshape(n, 3)
+    return tv, tn, np.array(g.areas, dtype=np.float64).reshape(n)
+
+
 class PackedScene:
     """Owns the numpy arrays a PtSceneDesc points into."""
 
     def __init__(self, scene):
         if scene.light_obj is None:
             raise ValueError("scene has no light (SDL `light` keyword)")
-        tris, norms, areas, obj_ids = [], [], [], []
         n_obj = len(scene.objects)
-        for oi, obj in enumerate(scene.objects):
-            g = obj['geometry']
-            for t, n, a in zip(g.triangles, g.normals, g.areas):
-                tris.append([v[:3] for v in t])
-                norms.append(n[:3])
-                areas.append(a)
-                obj_ids.append(oi)
-        self.n_obj_tri = len(tris)
-        lg = scene.light_obj
-        for t, n, a in zip(lg.triangles, lg.normals, lg.areas):
-            tris.append([v[:3] for v in t])
-            norms.append(n[:3])
-            areas.append(a)
-            obj_ids.append(n_obj)
-        if len(tris) == self.n_obj_tri:
+        geoms = [o['geometry'] for o in scene.objects] + [scene.light_obj]
+        parts = [_mesh_arrays(g) for g in geoms]
+        counts = [p[2].shape[0] for p in parts]
+        self.n_obj_tri = int(sum(counts[:-1]))
+        if counts[-1] == 0:
             raise ValueError("light object has no triangles")
         self.n_obj = n_obj
-        self.tri_v = np.ascontiguousarray(np.array(tris, dtype=np.float64).reshape(-1, 3, 3))
-        self.tri_n = np.ascontiguousarray(np.array(norms, dtype=np.float64).reshape(-1, 3))
-        self.tri_area = np.ascontiguousarray(np.array(areas, dtype=np.float64))
-        self.tri_obj = np.ascontiguousarray(np.array(obj_ids, dtype=np.int32))
+        self.tri_v = np.ascontiguousarray(np.concatenate([p[0] for p in parts]).reshape(-1, 3, 3))
+        self.tri_n = np.ascontiguousarray(np.concatenate([p[1] for p in parts]).reshape(-1, 3))
+        self.tri_area = np.ascontiguousarray(np.concatenate([p[2] for p in parts]))
+        self.tri_obj = np.ascontiguousarray(
+            np.repeat(np.arange(n_obj + 1, dtype=np.int32), counts).astype(np.int32))
         self.mat = np.ascontiguousarray(np.array(
             [[float(o[k]) for k in MAT_KEYS] for o in scene.objects],
             dtype=np.float64).reshape(-1, 8))

@@ -1,0 +1,168 @@
+"""Native OBJ reader (pt_obj_load) against the
+reference's Obj semantics (scene_reader.py:49-104, vector.py:143-173).
+
+The Python reader in scene_reader.py is the line-by-line restatement of the
+reference (pinned by the golden scene dump, test_oracle_golden.py); here the
+native reader must produce bit-identical vertices, normals and areas, the same
+list attributes, the same skipped-command messages, and — for inputs outside
+its subset — defer to the Python reader so the reference's exceptions are
+raised.  No GPU needed."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import CORNELL
+from pathtracerpython_amd import scene_reader
+from pathtracerpython_amd.pack import pack_scene
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture
+def quiet():
+    old = scene_reader.VERBOSE
+    scene_reader.VERBOSE = False
+    yield
+    scene_reader.VERBOSE = old
+
+
+def _read(path, native):
+    old = scene_reader.NATIVE_OBJ
+    scene_reader.NATIVE_OBJ = native
+    try:
+        return scene_reader.Obj(str(path))
+    finally:
+        scene_reader.NATIVE_OBJ = old
+
+
+def _same(a, b):
+    assert a.vertexes == b.vertexes
+    assert [list(f) for f in a.faces] == [list(f) for f in b.faces]
+    assert a.triangles == b.triangles
+    assert a.vtx_idx == b.vtx_idx
+    # bit-identical doubles (== would accept -0.0 vs 0.0; compare the bits)
+    an = np.array(a.normals, dtype=np.float64).reshape(-1, 3)
+    bn = np.array(b.normals, dtype=np.float64).reshape(-1, 3)
+    assert an.tobytes() == bn.tobytes()
+    assert np.array(a.areas, dtype=np.float64).tobytes() == np.array(b.areas, dtype=np.float64).tobytes()
+
+
+def test_cornell_native_equals_python(quiet):
+    base = os.path.dirname(CORNELL)
+    for f in sorted(os.listdir(base)):
+        if f.endswith(".obj"):
+            nat = _read(os.path.join(base, f), True)
+            assert nat.arrays is not None, f"{f}: native reader not used"
+            _same(nat, _read(os.path.join(base, f), False))
+
+
+def test_cornell_scene_matches_golden_dump(quiet):
+    g = np.load(os.path.join(GOLDEN, "scene_cornell.npz"))
+    pk = pack_scene(scene_reader.Scene(CORNELL))
+    assert pk.tri_v.tobytes() == np.ascontiguousarray(g["triangles"]).tobytes()
+    assert pk.tri_n.tobytes() == np.ascontiguousarray(g["normals"]).tobytes()
+    assert pk.tri_area.tobytes() == np.ascontiguousarray(g["areas"]).tobytes()
+
+
+EDGE = (
+    "# header comment\n"
+    "v 0 0 0\n"
+    "   v 1.5 0 0   # trailing comment\n"
+    "v\t0\t2.25\t0\r\n"
+    "v 1e-3 -2.5E+1 .5\r"
+    "v -0.0 3. +4\n"
+    "\n"
+    "vn 0 0 1\n"
+    "vt 0.5 0.5\n"
+    "g group one\n"
+    "usemtl white\n"
+    "f 1 2 3\n"
+    "f -1 -2 -3\n"
+    "f 1 2 3 4 5\n"
+    "f 0 2 3\n"          # index 0 -> -1: Python wraps to the last vertex
+    "f -5 4 +2\n"
+    "s off\n"
+    "v 7 7 7\n"
+    "f 6 1 3\n"
+    "   \n"
+    "f 1 3 2 # inline\n"
+)
+
+
+@pytest.mark.parametrize("newline", ["\n", "\r\n"])
+def test_edge_cases_native_equals_python(tmp_path, quiet, newline):
+    p = tmp_path / "edge.obj"
+    p.write_bytes(EDGE.replace("\n", newline).encode())
+    nat = _read(p, True)
+    assert nat.arrays is not None
+    _same(nat, _read(p, False))
+
+
+def test_skipped_command_messages_match(tmp_path, capsys):
+    p = tmp_path / "edge.obj"
+    p.write_text(EDGE)
+    scene_reader.VERBOSE = True
+    try:
+        _read(p, True)
+        out_native = capsys.readouterr().out
+        _read(p, False)
+        out_python = capsys.readouterr().out
+    finally:
+        scene_reader.VERBOSE = False
+    assert out_native == out_python
+    assert "Skipping command 'vn'" in out_native
+
+
+@pytest.mark.parametrize("text,exc", [
+    ("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1/1 2/2 3/3\n", ValueError),   # int('1/1')
+    ("v 0 0 0\nv 1 0 0\nv 2 0 0\nf 1 2 3\n", ZeroDivisionError),  # zero-area: 1/0
+    ("v 0 0 0\nv 1 0 0\nf 1 2\n", IndexError),                   # two indices
+    ("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 9\n", IndexError),         # out of range
+    ("v 0x1p0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3\n", ValueError),     # hex float
+])
+def test_outside_subset_raises_like_reference(tmp_path, quiet, text, exc):
+    p = tmp_path / "bad.obj"
+    p.write_text(text)
+    with pytest.raises(exc):
+        _read(p, True)
+    with pytest.raises(exc):
+        _read(p, False)
+
+
+def test_four_coordinate_vertices_fall_back(tmp_path, quiet):
+    p = tmp_path / "w.obj"
+    p.write_text("v 0 0 0 1\nv 1 0 0 1\nv 0 1 0 1\nf 1 2 3\n")
+    nat = _read(p, True)
+    assert nat.arrays is None          # Python reader took it
+    _same(nat, _read(p, False))
+
+
+def test_random_mesh_native_equals_python(tmp_path, quiet):
+    # K5-like small triangles: |cross| components where libm pow(c, 2) and
+    # c * c round differently occur often enough to catch a c * c shortcut
+    rs = np.random.RandomState(3)
+    n = 20000
+    v = (rs.uniform(-3, 3, (n, 1, 3)) + rs.normal(0, 0.05, (n, 3, 3))).reshape(-1, 3)
+    lines = ["v %.17g %.17g %.17g" % tuple(x) for x in v]
+    lines += ["f %d %d %d" % (3 * i + 1, 3 * i + 2, 3 * i + 3) for i in range(n)]
+    p = tmp_path / "rand.obj"
+    p.write_text("\n".join(lines) + "\n")
+    nat = _read(p, True)
+    assert nat.arrays["tri_v"].shape == (n, 3, 3)
+    _same(nat, _read(p, False))
+
+
+def test_k5_generator_ingests_identically(tmp_path, quiet):
+    from pathtracerpython_amd.synth import write_k5_scene
+    sdl = write_k5_scene(str(tmp_path), n_tris=4000, seed=0, size=64)
+    a = pack_scene(scene_reader.Scene(sdl))
+    old = scene_reader.NATIVE_OBJ
+    scene_reader.NATIVE_OBJ = False
+    try:
+        b = pack_scene(scene_reader.Scene(sdl))
+    finally:
+        scene_reader.NATIVE_OBJ = old
+    assert a.n_tri == 4000 + 10 + 2 and a.n_obj == 6
+    for k in ("tri_v", "tri_n", "tri_area", "tri_obj"):
+        assert getattr(a, k).tobytes() == getattr(b, k).tobytes(), k
