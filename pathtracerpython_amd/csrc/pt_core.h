@@ -95,8 +95,22 @@ struct alignas(16) Mat {
     int32_t pad[3];
 };
 
+// BVH node over the plane units of large meshes (pt_prepare.h): boxes in
+// centred f32 coordinates, inflated by a rigorous margin so that pruning with
+// the f32 line never drops a test the reference's f64 line would pass.
+// Depth-first layout with skip links (stackless traversal): an internal
+// node's first child is the next node; `skip` is the node after its subtree
+// (-1: done).  leaf >= 0: units [leaf >> 3, + (leaf & 7)) of SceneK::bunit.
+struct alignas(16) BNode {
+    float lo[3];
+    int32_t skip;
+    float hi[3];
+    int32_t leaf;
+};
+
 struct SceneK {
-    const UnitF* unit;          // [n_unit] plane units, object units first
+    const UnitF* unit;          // [n_unit] uniform plane units: object units (small objects, scene
+                                // order), then the light's; large meshes go to the BVH
     const TriD* trid;
     const TriS* tris;
     const int32_t* tri_obj;
@@ -106,6 +120,9 @@ struct SceneK {
     const int32_t* tri_grp;     // [n_tri] coplanar group of each triangle
     int32_t n_tri, n_obj_tri, n_obj, n_light;
     int32_t n_unit, n_obj_unit, pad0, pad1;
+    const BNode* bnode;         // [n_bnode] BVH of the mesh objects' units (none: n_bnode = 0)
+    const UnitF* bunit;         // [n_bunit] those units in leaf order
+    int32_t n_bnode, n_bunit, bvh_min_tri, pad2;   // bvh_min_tri: lowest triangle index in it
     double light_sum;
     double eye[3];
     double ortho[4];

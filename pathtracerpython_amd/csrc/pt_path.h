@@ -115,6 +115,56 @@ PT_HD void closest_unit(const SceneK& S, const UnitF& U, const OriginU& O, F3 d3
         closest_tri<COUNT>(S, U.tri[1], p, O.bo1, O.co1, d32, coplanar, sp, o_slot, dn_slot, acc, cnt);
 }
 
+// BVH helpers (the traversal itself, bvh_pass, follows fused_unit below)
+PT_HD F3 rcp_dir(F3 d) {   // 1/d; a zero component gives +-1e30 (finite: no 0 * inf)
+    F3 r;
+    r.x = 1.0f / (d.x == 0.0f ? 1e-30f : d.x);
+    r.y = 1.0f / (d.y == 0.0f ? 1e-30f : d.y);
+    r.z = 1.0f / (d.z == 0.0f ? 1e-30f : d.z);
+    return r;
+}
+// slab test of the line o + t d against a box given relative to o (lo - o,
+// hi - o): some |t| <= R inside (the line is two-sided, utils.py:118-120)
+PT_HD bool box_hit(F3 l, F3 h, F3 inv, float R) {
+    const float ax = l.x * inv.x, bx = h.x * inv.x;
+    const float ay = l.y * inv.y, by = h.y * inv.y;
+    const float az = l.z * inv.z, bz = h.z * inv.z;
+    const float tmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    return (tmin <= tmax) & (tmin <= R) & (tmax >= -R);
+}
+
+// f64 rescan of the BVH triangles within |t| <= R (an upper bound of the true
+// closest distance): the reference's closest hit, ties to the lower index
+PT_HD void bvh_rescan(const SceneK& S, D3 o, D3 dn, float R, int* best, double* bsq) {
+    const F3 o32 = to_f3(o - ld3(S.center));
+    const F3 inv = rcp_dir(to_f3(dn));
+    int node = 0;
+    while (node >= 0) {
+        const BNode N = S.bnode[node];
+        const F3 l = {N.lo[0] - o32.x, N.lo[1] - o32.y, N.lo[2] - o32.z};
+        const F3 h = {N.hi[0] - o32.x, N.hi[1] - o32.y, N.hi[2] - o32.z};
+        const bool hit = box_hit(l, h, inv, R);
+        if (hit && N.leaf >= 0) {
+            const int u0 = N.leaf >> 3, nu = N.leaf & 7;
+            for (int i = 0; i < nu; ++i) {
+                const UnitF& U = S.bunit[u0 + i];
+                for (int m = 0; m < U.count; ++m) {
+                    const int t = U.tri[m].t;
+                    D3 Q;
+                    double sqd;
+                    if (eval64(S.trid[t], o, dn, &Q, &sqd) && sqd > kZero &&
+                        (*best < 0 || sqd < *bsq || (sqd == *bsq && t < *best))) {
+                        *best = t;
+                        *bsq = sqd;
+                    }
+                }
+            }
+        }
+        node = (hit && N.leaf < 0) ? node + 1 : N.skip;
+    }
+}
+
 // Finish a closest-hit query: the candidate with the smallest lower bound is
 // certainly the closest when its interval ends before every other one
 // starts; otherwise rescan exactly in f64.  Returns the triangle (-1 = None)
@@ -128,12 +178,28 @@ PT_HD int closest_finish(const SceneK& S, const ClosestAcc& c, D3 o, D3 dn, D3* 
         if (!FORCE64) bump<COUNT>(cnt, &Counters::rescans, 1);
         best = -1;
         double bsq = 0.0;
-        for (int t = 0; t < S.n_tri; ++t) {
-            D3 Q; double sqd;
-            if (eval64(S.trid[t], o, dn, &Q, &sqd) && sqd > kZero && (best < 0 || sqd < bsq)) {
-                best = t;
-                bsq = sqd;
+        if (FORCE64 || S.n_bnode == 0) {
+            for (int t = 0; t < S.n_tri; ++t) {
+                D3 Q; double sqd;
+                if (eval64(S.trid[t], o, dn, &Q, &sqd) && sqd > kZero && (best < 0 || sqd < bsq)) {
+                    best = t;
+                    bsq = sqd;
+                }
             }
+        } else {   // the uniform units' triangles, then the BVH within |t| <= b1
+            for (int u = 0; u < S.n_unit; ++u) {
+                const UnitF& U = S.unit[u];
+                for (int m = 0; m < U.count; ++m) {
+                    const int t = U.tri[m].t;
+                    D3 Q; double sqd;
+                    if (eval64(S.trid[t], o, dn, &Q, &sqd) && sqd > kZero &&
+                        (best < 0 || sqd < bsq || (sqd == bsq && t < best))) {
+                        best = t;
+                        bsq = sqd;
+                    }
+                }
+            }
+            bvh_rescan(S, o, dn, c.b1, &best, &bsq);
         }
     }
     if (best >= 0) {
@@ -143,27 +209,6 @@ PT_HD int closest_finish(const SceneK& S, const ClosestAcc& c, D3 o, D3 dn, D3* 
     bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
     bump<COUNT>(cnt, &Counters::ray_bounces, 1);
     return best;
-}
-
-// Standalone query (primary rays, the batched intersect_objects API).  d need
-// not be normalised (utils.py:110).  ogrp: coplanar group of the triangle the
-// origin lies on (-1: none).
-template <bool FORCE64, bool COUNT>
-PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, const Spill& sp, D3* P, Counters* cnt) {
-    const D3 dn = unit(d);
-    ClosestAcc acc = closest_init();
-    if (!FORCE64) {
-        sp.put3(kSpP, o);
-        sp.put3(kSpNd, d);
-        const F3 o32 = to_f3(o - ld3(S.center));
-        const F3 d32 = to_f3(dn);
-        for (int u = 0; u < S.n_unit; ++u) {
-            const UnitF U = S.unit[u];
-            closest_unit<COUNT>(S, U, origin_u(U, o32), d32, U.grp == ogrp, sp, kSpP, kSpNd,
-                                &acc, cnt);
-        }
-    }
-    return closest_finish<FORCE64, COUNT>(S, acc, o, dn, P, cnt);
 }
 
 // ---------------------------------------------------------- direct light --
@@ -176,8 +221,8 @@ struct ShadowSet {
     F3 d32[kLightSamples];
     float hlo[kLightSamples], hhi[kLightSamples];
     bool occ[kLightSamples];
-    int first[kLightSamples];
-    int leak;
+    int first[kLightSamples];  // count mode: lowest occluding triangle (n_tri: none)
+    int last_first;            // lowest occluding triangle of the last ray (n_tri: none)
 };
 
 // Light sample k uses the uniforms of slots 4k..4k+3 (one Philox block: the
@@ -206,9 +251,9 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, u
         sh->hhi[k] = tl * (1.0f + 1e-6f);
         sh->d32[k] = to_f3(dn);
         sh->occ[k] = false;
-        sh->first[k] = S.n_obj_tri;
+        sh->first[k] = S.n_tri;
     }
-    sh->leak = S.n_obj - 1;
+    sh->last_first = S.n_tri;
 }
 
 // One plane unit against the 3 shadow rays and the next ray's closest hit,
@@ -216,10 +261,9 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, u
 // computed branch-free; ambiguous tests are only recorded as bits and
 // decided in f64 in one (rare) block per unit, so the common path carries no
 // per-test exec-mask juggling.  Scene order is kept where it matters: for
-// each shadow ray the unit's triangles are decided in order, and both
-// triangles of a unit belong to one object, so the leaked colour of
-// main.py:70 (object of the first occluder) does not depend on which of the
-// two decided first.
+// each shadow ray the lowest occluding triangle index is tracked, so the
+// leaked colour of main.py:70 (object of the first occluder in scene order)
+// does not depend on the order units are visited in.
 template <bool FORCE64, bool COUNT>
 PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
                       bool do_shadow, bool do_closest, ShadowSet* sh, F3 n32, ClosestAcc* ca,
@@ -245,11 +289,19 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
                     a1 = v1.amb & !coplanar;
                 }
             }
-            const bool newly = (!occ0[k]) & (c0 | c1);
-            if (COUNT && newly) sh->first[k] = (c0 ? U.tri[0].t : U.tri[1].t) + 1;
-            if (k == kLightSamples - 1 && newly) sh->leak = U.obj;
-            sh->occ[k] = occ0[k] | c0 | c1;
-            if (!occ0[k]) amb |= (a0 ? 1u : 0u) << (2 * k) | (a1 ? 2u : 0u) << (2 * k);
+            // which ambiguous tests still matter: rays 0, 1 until occluded (count
+            // mode: until their lowest occluder is known), the last ray until
+            // its lowest occluder is known (the leaked colour).  Units may come
+            // in any order (the BVH), so "first" is the lowest triangle index.
+            const int t0 = U.tri[0].t;
+            const bool need = (k == kLightSamples - 1) ? (t0 < sh->last_first)
+                              : (COUNT ? (t0 < sh->first[k]) : !occ0[k]);
+            const bool c = c0 | c1;
+            const int tc = c0 ? t0 : U.tri[1].t;
+            if (COUNT && c && tc < sh->first[k]) sh->first[k] = tc;
+            if (k == kLightSamples - 1 && c && tc < sh->last_first) sh->last_first = tc;
+            sh->occ[k] = occ0[k] | c;
+            if (need) amb |= (a0 ? 1u : 0u) << (2 * k) | (a1 ? 2u : 0u) << (2 * k);
         }
     }
     if (!FORCE64 && do_closest) {
@@ -275,14 +327,18 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
             for (int i = 0; i < 2; ++i) {
                 if (!((amb >> (2 * k + i)) & 1u)) continue;
                 const int t = U.tri[i].t;
+                // decided meanwhile (a lower occluder of this unit, or occlusion)?
+                if (k == kLightSamples - 1 ? (t >= sh->last_first)
+                                           : (COUNT ? (t >= sh->first[k]) : sh->occ[k]))
+                    continue;
                 D3 Q;
                 double sqd;
                 if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
                 const D3 L = sp.get3(kSpL + 3 * k);
                 if (eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
                     sqd < squared_dist(P, L)) {
-                    if (COUNT && (!sh->occ[k] || t + 1 < sh->first[k])) sh->first[k] = t + 1;
-                    if (k == kLightSamples - 1) sh->leak = S.tri_obj[t];
+                    if (COUNT && t < sh->first[k]) sh->first[k] = t;
+                    if (k == kLightSamples - 1) sh->last_first = t;
                     sh->occ[k] = true;
                 }
             }
@@ -312,15 +368,86 @@ PT_HD D3 shadow_color(const SceneK& S, D3 n, int obj, const ShadowSet& sh, const
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
         if (!sh.occ[k]) dsum += dot(unit(sp.get3(kSpL + 3 * k) - P), n);   // main.py:66-68
-        bump<COUNT>(cnt, &Counters::shadow_tests, (uint32_t)sh.first[k]);
+        // the reference's loop stops at the first occluder (main.py:42-55)
+        bump<COUNT>(cnt, &Counters::shadow_tests,
+                    (uint32_t)(sh.first[k] < S.n_tri ? sh.first[k] + 1 : S.n_obj_tri));
     }
     dsum /= (double)kLightSamples;
     const Mat& m = S.mat[obj];
-    const Mat& lm = S.mat[sh.leak];
+    // main.py:70: the object of the last ray's first occluder, else the last object
+    const Mat& lm = S.mat[sh.last_first < S.n_tri ? S.tri_obj[sh.last_first] : S.n_obj - 1];
     bump<COUNT>(cnt, &Counters::shading_points, 1);
     return d3(m.rgb[0] * m.ka * S.ambient + S.light_rgb[0] * lm.rgb[0] * dsum,
               m.rgb[1] * m.ka * S.ambient + S.light_rgb[1] * lm.rgb[1] * dsum,
               m.rgb[2] * m.ka * S.ambient + S.light_rgb[2] * lm.rgb[2] * dsum);
+}
+
+// ------------------------------------------------------------------ BVH --
+// Large meshes (SceneK::bnode/bunit, built in pt_prepare.h).  One stackless
+// traversal per lane and bounce serves all four lines of the fused pass: a
+// node is entered when one of them meets its box within its range (shadow
+// ray k: |t| <= hhi[k]; the closest ray: |t| <= the current best's upper
+// bound), and its leaf units go through fused_unit like the uniform ones.
+template <bool FORCE64, bool COUNT>
+PT_HD void bvh_pass(const SceneK& S, F3 o32, int ogrp, bool do_shadow, bool do_closest,
+                    ShadowSet* sh, F3 n32, ClosestAcc* ca, const Spill& sp, Counters* cnt) {
+    F3 inv[kLightSamples];
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) inv[k] = rcp_dir(sh->d32[k]);
+    const F3 invc = rcp_dir(n32);
+    int node = (do_shadow || do_closest) ? 0 : -1;
+    while (node >= 0) {
+        const BNode N = S.bnode[node];
+        const F3 l = {N.lo[0] - o32.x, N.lo[1] - o32.y, N.lo[2] - o32.z};
+        const F3 h = {N.hi[0] - o32.x, N.hi[1] - o32.y, N.hi[2] - o32.z};
+        bool hit = false;
+        if (do_shadow) {
+#pragma unroll
+            for (int k = 0; k < kLightSamples; ++k) {
+                // rays still open: 0, 1 until occluded (count mode: until no BVH
+                // triangle can be their lowest occluder); the last ray likewise
+                const bool open = (k == kLightSamples - 1) ? (sh->last_first > S.bvh_min_tri)
+                                  : (COUNT ? (sh->first[k] > S.bvh_min_tri) : !sh->occ[k]);
+                hit |= open && box_hit(l, h, inv[k], sh->hhi[k]);
+            }
+        }
+        if (do_closest) hit |= box_hit(l, h, invc, ca->b1);
+        if (hit && N.leaf >= 0) {
+            const int u0 = N.leaf >> 3, nu = N.leaf & 7;
+            for (int i = 0; i < nu; ++i) {
+                const UnitF U = S.bunit[u0 + i];
+                const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
+                fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, do_shadow, do_closest, sh, n32,
+                                           ca, sp, cnt);
+            }
+        }
+        node = (hit && N.leaf < 0) ? node + 1 : N.skip;
+    }
+}
+
+// Standalone query (primary rays, the batched intersect_objects API).  d need
+// not be normalised (utils.py:110).  ogrp: coplanar group of the triangle the
+// origin lies on (-1: none).
+template <bool FORCE64, bool COUNT>
+PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, const Spill& sp, D3* P, Counters* cnt) {
+    const D3 dn = unit(d);
+    ClosestAcc acc = closest_init();
+    if (!FORCE64) {
+        sp.put3(kSpP, o);
+        sp.put3(kSpNd, d);
+        const F3 o32 = to_f3(o - ld3(S.center));
+        const F3 d32 = to_f3(dn);
+        for (int u = 0; u < S.n_unit; ++u) {
+            const UnitF U = S.unit[u];
+            closest_unit<COUNT>(S, U, origin_u(U, o32), d32, U.grp == ogrp, sp, kSpP, kSpNd,
+                                &acc, cnt);
+        }
+        if (S.n_bnode) {   // the meshes: closest ray only
+            ShadowSet none = {};
+            bvh_pass<false, COUNT>(S, o32, ogrp, false, true, &none, d32, &acc, sp, cnt);
+        }
+    }
+    return closest_finish<FORCE64, COUNT>(S, acc, o, dn, P, cnt);
 }
 
 // Standalone compute_color (batched API): u = the 12 light-sampling uniforms.
@@ -338,6 +465,8 @@ PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
         fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, true, false, &sh, F3{0.f, 0.f, 0.f},
                                    nullptr, sp, cnt);
     }
+    if (S.n_bnode)
+        bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, false, &sh, F3{0.f, 0.f, 0.f}, nullptr, sp, cnt);
     return shadow_color<COUNT>(S, n, obj, sh, sp, cnt);
 }
 
@@ -459,6 +588,8 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
             fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
                                        &ca, sp, cnt);
         }
+        if (S.n_bnode)   // the meshes
+            bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, !FORCE64 && trace, &sh, n32, &ca, sp, cnt);
         if (!FORCE64 && any_trace) {
             for (int u = S.n_obj_unit; u < S.n_unit; ++u) {   // the light's units
                 const UnitF U = S.unit[u];

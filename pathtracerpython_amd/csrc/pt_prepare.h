@@ -18,6 +18,8 @@ namespace pt {
 
 struct HostScene {
     std::vector<UnitF> unit;
+    std::vector<UnitF> bunit;
+    std::vector<BNode> bnode;
     std::vector<int32_t> tri_grp;
     std::vector<TriD> trid;
     std::vector<TriS> tris;
@@ -27,6 +29,167 @@ struct HostScene {
     std::vector<double> light_cum;
     SceneK k{};   // pointers unset; constants filled
 };
+
+constexpr int kBvhMinTris = 64;   // objects this large are traversed through the BVH
+constexpr int kBvhLeaf = 4;       // units per leaf (at most 7: 3 bits of BNode::leaf)
+constexpr int kBvhBins = 16;
+
+// outward rounding to f32
+inline float f32_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = nextafterf(f, -INFINITY);
+    return f;
+}
+inline float f32_upb(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = nextafterf(f, INFINITY);
+    return f;
+}
+
+// Binned-SAH BVH over H->bunit (reordered into leaf order), depth-first with
+// skip links.  Unit boxes are in centred coordinates, inflated by
+// delta = 64 u X: the f32 line the kernel traverses with (centred origin and
+// direction rounded to f32) stays within ~20 u X of the exact line for every
+// |t| <= 2 sqrt(3) X, slab arithmetic included, so a box test with the f32
+// line never rejects a unit the exact line meets.
+struct BvhBuilder {
+    struct Item { double lo[3], hi[3], c[3]; };
+    HostScene* H;
+    double delta;
+    std::vector<Item> it;
+    std::vector<int> idx;
+    std::vector<UnitF> ordered;
+
+    static double area(const double* lo, const double* hi) {
+        const double e0 = hi[0] - lo[0], e1 = hi[1] - lo[1], e2 = hi[2] - lo[2];
+        return (e0 < 0 || e1 < 0 || e2 < 0) ? 0.0 : 2 * (e0 * e1 + e1 * e2 + e2 * e0);
+    }
+    int bin_of(double c, double lo, double ext) const {
+        int q = (int)((c - lo) / ext * kBvhBins);
+        return std::min(std::max(q, 0), kBvhBins - 1);
+    }
+    // SAH split position in [b, e) (partitions idx), or -1 for a leaf
+    int split(int b, int e) {
+        if (e - b <= kBvhLeaf) return -1;
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = b; i < e; ++i)
+            for (int a = 0; a < 3; ++a) {
+                clo[a] = std::min(clo[a], it[idx[i]].c[a]);
+                chi[a] = std::max(chi[a], it[idx[i]].c[a]);
+            }
+        double best = INFINITY;
+        int best_axis = -1, best_bin = -1;
+        for (int a = 0; a < 3; ++a) {
+            const double ext = chi[a] - clo[a];
+            if (!(ext > 0)) continue;
+            int bc[kBvhBins] = {0};
+            double blo[kBvhBins][3], bhi[kBvhBins][3];
+            for (int q = 0; q < kBvhBins; ++q)
+                for (int z = 0; z < 3; ++z) { blo[q][z] = INFINITY; bhi[q][z] = -INFINITY; }
+            for (int i = b; i < e; ++i) {
+                const Item& I = it[idx[i]];
+                const int q = bin_of(I.c[a], clo[a], ext);
+                bc[q]++;
+                for (int z = 0; z < 3; ++z) {
+                    blo[q][z] = std::min(blo[q][z], I.lo[z]);
+                    bhi[q][z] = std::max(bhi[q][z], I.hi[z]);
+                }
+            }
+            double la[kBvhBins], lc[kBvhBins];
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            int c = 0;
+            for (int q = 0; q < kBvhBins - 1; ++q) {   // left of boundary q+1
+                c += bc[q];
+                for (int z = 0; z < 3; ++z) { lo[z] = std::min(lo[z], blo[q][z]); hi[z] = std::max(hi[z], bhi[q][z]); }
+                la[q] = area(lo, hi);
+                lc[q] = c;
+            }
+            for (int z = 0; z < 3; ++z) { lo[z] = INFINITY; hi[z] = -INFINITY; }
+            c = 0;
+            for (int q = kBvhBins - 1; q > 0; --q) {   // right of boundary q
+                c += bc[q];
+                for (int z = 0; z < 3; ++z) { lo[z] = std::min(lo[z], blo[q][z]); hi[z] = std::max(hi[z], bhi[q][z]); }
+                const double cost = la[q - 1] * lc[q - 1] + area(lo, hi) * c;
+                if (lc[q - 1] > 0 && c > 0 && cost < best) { best = cost; best_axis = a; best_bin = q; }
+            }
+        }
+        int mid = -1;
+        if (best_axis >= 0) {
+            const int a = best_axis;
+            const double lo = clo[a], ext = chi[a] - clo[a];
+            mid = (int)(std::partition(idx.begin() + b, idx.begin() + e,
+                                       [&](int i) { return bin_of(it[i].c[a], lo, ext) < best_bin; }) -
+                        idx.begin());
+        }
+        if (mid <= b || mid >= e) mid = (b + e) / 2;   // coincident centroids: halve
+        return mid;
+    }
+    int build(int b, int e) {   // returns the subtree's root node
+        BNode N{};
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = b; i < e; ++i)
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], it[idx[i]].lo[a]);
+                hi[a] = std::max(hi[a], it[idx[i]].hi[a]);
+            }
+        for (int a = 0; a < 3; ++a) {
+            N.lo[a] = f32_down(lo[a] - delta);
+            N.hi[a] = f32_upb(hi[a] + delta);
+        }
+        N.leaf = -1;
+        const int node = (int)H->bnode.size();
+        H->bnode.push_back(N);
+        const int mid = split(b, e);
+        if (mid < 0) {
+            H->bnode[node].leaf = ((int32_t)ordered.size() << 3) | (e - b);
+            for (int i = b; i < e; ++i) ordered.push_back(H->bunit[idx[i]]);
+        } else {
+            build(b, mid);
+            build(mid, e);
+        }
+        H->bnode[node].skip = (int)H->bnode.size();   // the node after this subtree
+        return node;
+    }
+};
+
+inline void build_bvh(HostScene* H, double X) {
+    H->bnode.clear();
+    SceneK& K = H->k;
+    K.n_bnode = 0;
+    K.n_bunit = (int32_t)H->bunit.size();
+    K.bvh_min_tri = K.n_tri;
+    const int n = (int)H->bunit.size();
+    if (n == 0) return;
+    BvhBuilder B;
+    B.H = H;
+    B.delta = 64.0 / 16777216.0 * X;
+    B.it.resize(n);
+    for (int i = 0; i < n; ++i) {
+        const UnitF& U = H->bunit[i];
+        BvhBuilder::Item& I = B.it[i];
+        for (int a = 0; a < 3; ++a) { I.lo[a] = INFINITY; I.hi[a] = -INFINITY; }
+        for (int m = 0; m < U.count; ++m) {
+            const TriD& T = H->trid[U.tri[m].t];
+            K.bvh_min_tri = std::min(K.bvh_min_tri, U.tri[m].t);
+            const double* vs[3] = {T.v1, T.v2, T.v3};
+            for (int v = 0; v < 3; ++v)
+                for (int a = 0; a < 3; ++a) {
+                    const double x = vs[v][a] - K.center[a];
+                    I.lo[a] = std::min(I.lo[a], x);
+                    I.hi[a] = std::max(I.hi[a], x);
+                }
+        }
+        for (int a = 0; a < 3; ++a) I.c[a] = 0.5 * (I.lo[a] + I.hi[a]);
+        B.idx.push_back(i);
+    }
+    B.ordered.reserve(n);
+    B.build(0, n);
+    const int total = (int)H->bnode.size();
+    for (BNode& N : H->bnode)
+        if (N.skip >= total) N.skip = -1;
+    H->bunit.swap(B.ordered);
+    K.n_bnode = total;
+}
 
 inline D3 tri_vertex(const pt_scene_desc* d, int t, int v) {
     return ld3(d->tri_v + 9 * t + 3 * v);
@@ -193,7 +356,13 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     // plane units: consecutive triangles of one object in one coplanar group
     // share a unit (at most 2).  The unit's plane is its first triangle's; the
     // members' planes agree to 1e-12 over the box, covered by +1e-9 slack.
+    // Objects with at least kBvhMinTris triangles ("meshes") go to the BVH;
+    // the others stay in the uniform list every lane walks in scene order.
+    std::vector<int32_t> obj_ntri(d->n_obj, 0);
+    for (int t = 0; t < d->n_obj_tri; ++t) obj_ntri[d->tri_obj[t]]++;
+    auto in_bvh = [&](int t) { return t < d->n_obj_tri && obj_ntri[d->tri_obj[t]] >= kBvhMinTris; };
     H->unit.clear();
+    H->bunit.clear();
     for (int part = 0; part < 2; ++part) {
         const int t_begin = part == 0 ? 0 : d->n_obj_tri, t_end = part == 0 ? d->n_obj_tri : T;
         for (int t = t_begin; t < t_end;) {
@@ -229,7 +398,7 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
                 U.eq = f32_up(eq);
                 U.qhi = f32_up((1e-5 + eq) * (1 + 1e-4));
             }
-            H->unit.push_back(U);
+            (in_bvh(t) ? H->bunit : H->unit).push_back(U);
             t += U.count;
         }
         if (part == 0) H->k.n_obj_unit = (int32_t)H->unit.size();
@@ -268,12 +437,15 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     }
     for (int i = 0; i < 4; ++i) K.ortho[i] = d->ortho[i];
     K.ambient = d->ambient;
+    build_bvh(H, X);   // needs K.center and K.n_tri
     return "";
 }
 
 // host pointers (for the host-side check build)
 inline void bind_host(HostScene* H) {
     H->k.unit = H->unit.data();
+    H->k.bnode = H->bnode.data();
+    H->k.bunit = H->bunit.data();
     H->k.tri_grp = H->tri_grp.data();
     H->k.trid = H->trid.data();
     H->k.tris = H->tris.data();

@@ -100,8 +100,8 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
         const F3 o32 = to_f3(o - C), d32 = to_f3(dn);
         const double lim = 0.5 + 40.0 * U(rng);   // a shadow range
         const float hlo = (float)(sqrt(lim) * (1 - 1e-6)), hhi = (float)(sqrt(lim) * (1 + 1e-6));
-        for (int u = 0; u < H.k.n_unit; ++u) {
-            const UnitF& U = H.unit[u];
+        for (int u = 0; u < H.k.n_unit + H.k.n_bunit; ++u) {   // uniform and BVH units
+            const UnitF& U = u < H.k.n_unit ? H.unit[u] : H.bunit[u - H.k.n_unit];
             const OriginU O = origin_u(U, o32);
             const RayPlane pc = ray_plane(U, O.h, d32, INFINITY, INFINITY);
             const RayPlane ps = ray_plane(U, O.h, d32, hlo, hhi);
@@ -131,6 +131,99 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
         }
     }
     out[0] = wrong; out[1] = amb; out[2] = tests; out[3] = cand;
+    return 0;
+}
+
+// BVH check.  Structure: every BVH unit in exactly one leaf, child boxes
+// inside their parent's, every triangle vertex inside its leaf's box, skip
+// links consistent with the depth-first layout.  Conservativeness: random
+// lines (as in the filter self-test); for every BVH triangle the f64
+// reference says the line meets at sqd, a traversal with the kernel's f32
+// line and range sqrt(sqd) (1 + 1e-6) must reach that triangle's leaf.
+// out: [0] structural errors, [1] missed hits, [2] hits checked, [3] nodes.
+int hc_bvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t* out) {
+    HostScene H;
+    if (!prepare_scene(d, &H).empty()) return -1;
+    bind_host(&H);
+    const SceneK& K = H.k;
+    int64_t bad = 0, missed = 0, checked = 0;
+    const int N = K.n_bnode;
+    std::vector<int> seen(K.n_bunit, 0), leaf_of(K.n_bunit, -1);
+    // structure: parent of node i+1 is i when i is internal; check via a stack walk
+    std::vector<int> st;
+    for (int i = 0; i < N; ++i) {
+        const BNode& B = H.bnode[i];
+        for (int a = 0; a < 3; ++a)
+            if (!(B.lo[a] <= B.hi[a])) ++bad;
+        if (B.leaf >= 0) {
+            const int u0 = B.leaf >> 3, nu = B.leaf & 7;
+            if (nu < 1 || u0 + nu > K.n_bunit) { ++bad; continue; }
+            if (B.skip != (i + 1 < N ? i + 1 : -1)) ++bad;
+            for (int q = u0; q < u0 + nu; ++q) {
+                seen[q]++;
+                leaf_of[q] = i;
+                const UnitF& U = H.bunit[q];
+                for (int m = 0; m < U.count; ++m) {
+                    const TriD& T = H.trid[U.tri[m].t];
+                    const double* vs[3] = {T.v1, T.v2, T.v3};
+                    for (int v = 0; v < 3; ++v)
+                        for (int a = 0; a < 3; ++a) {
+                            const double x = vs[v][a] - K.center[a];
+                            if (!(B.lo[a] <= x && x <= B.hi[a])) ++bad;
+                        }
+                }
+            }
+        } else {
+            if (i + 1 >= N) { ++bad; continue; }
+            const BNode& C = H.bnode[i + 1];   // first child
+            for (int a = 0; a < 3; ++a)
+                if (!(B.lo[a] <= C.lo[a] && C.hi[a] <= B.hi[a])) ++bad;
+            if (!(B.skip == -1 || (B.skip > i + 1 && B.skip <= N))) ++bad;
+        }
+    }
+    for (int q = 0; q < K.n_bunit; ++q)
+        if (seen[q] != 1) ++bad;
+    // conservativeness
+    std::mt19937_64 rng(seed);
+    std::uniform_real_distribution<double> U01(0.0, 1.0);
+    std::vector<char> visited(N);
+    for (int64_t r = 0; r < n_rays && K.n_bunit > 0; ++r) {
+        // origin: a point on a random BVH triangle or at the eye; random direction
+        D3 o;
+        if (r % 4 == 0) {
+            o = ld3(K.eye);
+        } else {
+            const UnitF& U = H.bunit[(size_t)(U01(rng) * K.n_bunit) % K.n_bunit];
+            const TriD& T = H.trid[U.tri[0].t];
+            double a = U01(rng), b = U01(rng);
+            if (a + b > 1) { a = 1 - a; b = 1 - b; }
+            o = ld3(T.v1) * (1 - a - b) + ld3(T.v2) * a + ld3(T.v3) * b;
+        }
+        D3 dir = d3(U01(rng) - 0.5, U01(rng) - 0.5, U01(rng) - 0.5);
+        const D3 dn = unit(dir);
+        const F3 o32 = to_f3(o - ld3(K.center)), inv = rcp_dir(to_f3(dn));
+        for (int q = 0; q < K.n_bunit; ++q) {
+            const UnitF& U = H.bunit[q];
+            for (int m = 0; m < U.count; ++m) {
+                D3 Q; double sqd;
+                if (!eval64(H.trid[U.tri[m].t], o, dn, &Q, &sqd)) continue;
+                const float R = (float)(sqrt(sqd) * (1 + 1e-6));
+                ++checked;
+                std::fill(visited.begin(), visited.end(), 0);
+                int node = 0;
+                while (node >= 0) {
+                    const BNode& B = H.bnode[node];
+                    const F3 l = {B.lo[0] - o32.x, B.lo[1] - o32.y, B.lo[2] - o32.z};
+                    const F3 h = {B.hi[0] - o32.x, B.hi[1] - o32.y, B.hi[2] - o32.z};
+                    const bool hit = box_hit(l, h, inv, R);
+                    if (hit) visited[node] = 1;
+                    node = (hit && B.leaf < 0) ? node + 1 : B.skip;
+                }
+                if (!visited[leaf_of[q]]) ++missed;
+            }
+        }
+    }
+    out[0] = bad; out[1] = missed; out[2] = checked; out[3] = N;
     return 0;
 }
 
