@@ -136,7 +136,7 @@ def main():
         roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                     "traffic": traffic,
-                    "kernel": "k_render<false,false>",
+                    "kernel": "k_render<false,false,false>",
                     "compute_pipe": "VALU f32 (no MFMA: scalar intersection; the MI355X f32 "
                                     "vector peak equals the f32 MFMA dense peak)",
                     "work_per_launch": {"ray_triangle_tests": tests,

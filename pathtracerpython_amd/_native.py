@@ -40,7 +40,11 @@ def _bind(lib):
         "pt_obj_load": ([C.c_char_p, C.POINTER(C.POINTER(PtMesh))], C.c_int),
         "pt_mesh_free": ([C.POINTER(PtMesh)], None),
     }
+    # PT_DEV_OLD_LIB=1 (dev sweeps only): bind what an older build exports
+    lenient = os.environ.get("PT_DEV_OLD_LIB") == "1"
     for name, (args, res) in sig.items():
+        if lenient and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res

@@ -63,7 +63,7 @@ __device__ __forceinline__ void flush_counters(const Counters& c, StatsDev* st) 
     }
 }
 
-template <bool FORCE64, bool COUNT>
+template <bool FORCE64, bool COUNT, bool BVH>
 // 4 waves/SIMD (<= 128 VGPRs, a little scratch spill outside the triangle
 // loops): 9.5 ms vs 10.8 ms at 3 waves and 15.3 ms at 2 on the 512^2 x 64spp
 // bench (MI355X), see DESIGN.md §5.
@@ -98,8 +98,8 @@ __global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __
         J.rr_depth = R.rr_depth;
         D3 P0 = d3(0, 0, 0);
         int tri0 = -1;
-        if (ns > 0 && R.bounces > 0) tri0 = closest<FORCE64, false>(S, eye, d0, -1, sp, &P0, &cnt);
-        acc = render_lane<FORCE64, COUNT>(S, J, d0, tri0, P0, sp, &cnt);
+        if (ns > 0 && R.bounces > 0) tri0 = closest<FORCE64, false, BVH>(S, eye, d0, -1, sp, &P0, &cnt);
+        acc = render_lane<FORCE64, COUNT, BVH>(S, J, d0, tri0, P0, sp, &cnt);
     }
     for (uint32_t m = 1; m < R.split; m <<= 1) {
         acc.x += __shfl_xor(acc.x, (int)m);
@@ -361,11 +361,14 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     if (count) HIPCHK(hipMemsetAsync(s->stats, 0, sizeof(StatsDev), st));
     HIPCHK(hipEventRecord(s->ev0, st));
     if (f64) {
-        if (count) hipLaunchKernelGGL((k_render<true, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
-        else hipLaunchKernelGGL((k_render<true, false>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+        if (count) hipLaunchKernelGGL((k_render<true, true, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+        else hipLaunchKernelGGL((k_render<true, false, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+    } else if (s->dev.n_bnode > 0) {   // scenes with meshes: the BVH instantiation
+        if (count) hipLaunchKernelGGL((k_render<false, true, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+        else hipLaunchKernelGGL((k_render<false, false, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
     } else {
-        if (count) hipLaunchKernelGGL((k_render<false, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
-        else hipLaunchKernelGGL((k_render<false, false>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+        if (count) hipLaunchKernelGGL((k_render<false, true, false>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+        else hipLaunchKernelGGL((k_render<false, false, false>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(s->ev1, st));

@@ -169,7 +169,7 @@ PT_HD void bvh_rescan(const SceneK& S, D3 o, D3 dn, float R, int* best, double* 
 // certainly the closest when its interval ends before every other one
 // starts; otherwise rescan exactly in f64.  Returns the triangle (-1 = None)
 // and the hit point exactly as the reference computes it.
-template <bool FORCE64, bool COUNT>
+template <bool FORCE64, bool COUNT, bool BVH = true>
 PT_HD int closest_finish(const SceneK& S, const ClosestAcc& c, D3 o, D3 dn, D3* P,
                          Counters* cnt) {
     int best = c.i1;
@@ -178,7 +178,7 @@ PT_HD int closest_finish(const SceneK& S, const ClosestAcc& c, D3 o, D3 dn, D3* 
         if (!FORCE64) bump<COUNT>(cnt, &Counters::rescans, 1);
         best = -1;
         double bsq = 0.0;
-        if (FORCE64 || S.n_bnode == 0) {
+        if (FORCE64 || !BVH || S.n_bnode == 0) {
             for (int t = 0; t < S.n_tri; ++t) {
                 D3 Q; double sqd;
                 if (eval64(S.trid[t], o, dn, &Q, &sqd) && sqd > kZero && (best < 0 || sqd < bsq)) {
@@ -395,25 +395,36 @@ PT_HD void bvh_pass(const SceneK& S, F3 o32, int ogrp, bool do_shadow, bool do_c
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) inv[k] = rcp_dir(sh->d32[k]);
     const F3 invc = rcp_dir(n32);
+    // "while-while": each lane walks internal nodes on its own until it finds
+    // a leaf its lines reach, then the lanes test their leaves together
     int node = (do_shadow || do_closest) ? 0 : -1;
     while (node >= 0) {
-        const BNode N = S.bnode[node];
-        const F3 l = {N.lo[0] - o32.x, N.lo[1] - o32.y, N.lo[2] - o32.z};
-        const F3 h = {N.hi[0] - o32.x, N.hi[1] - o32.y, N.hi[2] - o32.z};
-        bool hit = false;
-        if (do_shadow) {
+        int leaf = -1;
+        while (node >= 0) {
+            const BNode N = S.bnode[node];
+            const F3 l = {N.lo[0] - o32.x, N.lo[1] - o32.y, N.lo[2] - o32.z};
+            const F3 h = {N.hi[0] - o32.x, N.hi[1] - o32.y, N.hi[2] - o32.z};
+            bool hit = false;
+            if (do_shadow) {
 #pragma unroll
-            for (int k = 0; k < kLightSamples; ++k) {
-                // rays still open: 0, 1 until occluded (count mode: until no BVH
-                // triangle can be their lowest occluder); the last ray likewise
-                const bool open = (k == kLightSamples - 1) ? (sh->last_first > S.bvh_min_tri)
-                                  : (COUNT ? (sh->first[k] > S.bvh_min_tri) : !sh->occ[k]);
-                hit |= open && box_hit(l, h, inv[k], sh->hhi[k]);
+                for (int k = 0; k < kLightSamples; ++k) {
+                    // rays still open: 0, 1 until occluded (count mode: until no BVH
+                    // triangle can be their lowest occluder); the last ray likewise
+                    const bool open = (k == kLightSamples - 1) ? (sh->last_first > S.bvh_min_tri)
+                                      : (COUNT ? (sh->first[k] > S.bvh_min_tri) : !sh->occ[k]);
+                    hit |= open && box_hit(l, h, inv[k], sh->hhi[k]);
+                }
             }
+            if (do_closest) hit |= box_hit(l, h, invc, ca->b1);
+            if (hit && N.leaf >= 0) {
+                leaf = N.leaf;
+                node = N.skip;
+                break;
+            }
+            node = hit ? node + 1 : N.skip;
         }
-        if (do_closest) hit |= box_hit(l, h, invc, ca->b1);
-        if (hit && N.leaf >= 0) {
-            const int u0 = N.leaf >> 3, nu = N.leaf & 7;
+        if (leaf >= 0) {
+            const int u0 = leaf >> 3, nu = leaf & 7;
             for (int i = 0; i < nu; ++i) {
                 const UnitF U = S.bunit[u0 + i];
                 const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
@@ -421,14 +432,14 @@ PT_HD void bvh_pass(const SceneK& S, F3 o32, int ogrp, bool do_shadow, bool do_c
                                            ca, sp, cnt);
             }
         }
-        node = (hit && N.leaf < 0) ? node + 1 : N.skip;
     }
 }
 
 // Standalone query (primary rays, the batched intersect_objects API).  d need
 // not be normalised (utils.py:110).  ogrp: coplanar group of the triangle the
 // origin lies on (-1: none).
-template <bool FORCE64, bool COUNT>
+// BVH = false: the instantiation for scenes without meshes (no BVH code)
+template <bool FORCE64, bool COUNT, bool BVH = true>
 PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, const Spill& sp, D3* P, Counters* cnt) {
     const D3 dn = unit(d);
     ClosestAcc acc = closest_init();
@@ -442,16 +453,16 @@ PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, const Spill& sp, D3* P,
             closest_unit<COUNT>(S, U, origin_u(U, o32), d32, U.grp == ogrp, sp, kSpP, kSpNd,
                                 &acc, cnt);
         }
-        if (S.n_bnode) {   // the meshes: closest ray only
+        if (BVH && S.n_bnode) {   // the meshes: closest ray only
             ShadowSet none = {};
             bvh_pass<false, COUNT>(S, o32, ogrp, false, true, &none, d32, &acc, sp, cnt);
         }
     }
-    return closest_finish<FORCE64, COUNT>(S, acc, o, dn, P, cnt);
+    return closest_finish<FORCE64, COUNT, BVH>(S, acc, o, dn, P, cnt);
 }
 
 // Standalone compute_color (batched API): u = the 12 light-sampling uniforms.
-template <bool FORCE64, bool COUNT>
+template <bool FORCE64, bool COUNT, bool BVH = true>
 PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
              const Spill& sp, Counters* cnt) {
     ShadowSet sh;
@@ -465,7 +476,7 @@ PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
         fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, true, false, &sh, F3{0.f, 0.f, 0.f},
                                    nullptr, sp, cnt);
     }
-    if (S.n_bnode)
+    if (BVH && S.n_bnode)
         bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, false, &sh, F3{0.f, 0.f, 0.f}, nullptr, sp, cnt);
     return shadow_color<COUNT>(S, n, obj, sh, sp, cnt);
 }
@@ -520,7 +531,7 @@ struct LaneJob {
 // sample from the cached primary hit (primary rays are identical for every
 // sample, main.py:191), so a wave keeps tracing until all its lanes are out
 // of samples.
-template <bool FORCE64, bool COUNT>
+template <bool FORCE64, bool COUNT, bool BVH = true>
 PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
                      const Spill& sp, Counters* cnt) {
     D3 acc = d3(0, 0, 0);
@@ -588,7 +599,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
             fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
                                        &ca, sp, cnt);
         }
-        if (S.n_bnode)   // the meshes
+        if (BVH && S.n_bnode)   // the meshes
             bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, !FORCE64 && trace, &sh, n32, &ca, sp, cnt);
         if (!FORCE64 && any_trace) {
             for (int u = S.n_obj_unit; u < S.n_unit; ++u) {   // the light's units
@@ -604,7 +615,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         bool done = !trace;
         if (trace) {
             D3 Pn;
-            const int tn = closest_finish<FORCE64, COUNT>(S, ca, sp.get3(kSpP),
+            const int tn = closest_finish<FORCE64, COUNT, BVH>(S, ca, sp.get3(kSpP),
                                                           unit(sp.get3(kSpNd)), &Pn, cnt);
             if (tn < 0) {
                 bump<COUNT>(cnt, &Counters::escapes, 1);
