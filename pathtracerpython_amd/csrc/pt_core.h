@@ -120,15 +120,15 @@ struct SceneK {
     const int32_t* tri_grp;     // [n_tri] coplanar group of each triangle
     int32_t n_tri, n_obj_tri, n_obj, n_light;
     int32_t n_unit, n_obj_unit, pad0, pad1;
-    const BNode* bnode;         // [n_bnode] BVH of the mesh objects' units (none: n_bnode = 0)
-    const UnitF* bunit;         // [n_bunit] those units in leaf order
-    int32_t n_bnode, n_bunit, bvh_min_tri, pad2;   // bvh_min_tri: lowest triangle index in it
     double light_sum;
     double eye[3];
     double ortho[4];
     double ambient;
     double light_rgb[3];
     double center[3];
+    const BNode* bnode;         // [n_bnode] BVH of the mesh objects' units (none: n_bnode = 0)
+    const UnitF* bunit;         // [n_bunit] those units in leaf order
+    int32_t n_bnode, n_bunit, bvh_min_tri, pad2;   // bvh_min_tri: lowest triangle index in it
 };
 
 // ------------------------------------------------------------------ RNG --

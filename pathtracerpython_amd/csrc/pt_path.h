@@ -223,6 +223,7 @@ struct ShadowSet {
     bool occ[kLightSamples];
     int first[kLightSamples];  // count mode: lowest occluding triangle (n_tri: none)
     int last_first;            // lowest occluding triangle of the last ray (n_tri: none)
+    int leak;                  // its object (main.py:70), the last object when none
 };
 
 // Light sample k uses the uniforms of slots 4k..4k+3 (one Philox block: the
@@ -254,6 +255,7 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, u
         sh->first[k] = S.n_tri;
     }
     sh->last_first = S.n_tri;
+    sh->leak = S.n_obj - 1;
 }
 
 // One plane unit against the 3 shadow rays and the next ray's closest hit,
@@ -299,7 +301,10 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
             const bool c = c0 | c1;
             const int tc = c0 ? t0 : U.tri[1].t;
             if (COUNT && c && tc < sh->first[k]) sh->first[k] = tc;
-            if (k == kLightSamples - 1 && c && tc < sh->last_first) sh->last_first = tc;
+            if (k == kLightSamples - 1 && c && tc < sh->last_first) {
+                sh->last_first = tc;
+                sh->leak = U.obj;
+            }
             sh->occ[k] = occ0[k] | c;
             if (need) amb |= (a0 ? 1u : 0u) << (2 * k) | (a1 ? 2u : 0u) << (2 * k);
         }
@@ -338,7 +343,10 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
                 if (eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
                     sqd < squared_dist(P, L)) {
                     if (COUNT && t < sh->first[k]) sh->first[k] = t;
-                    if (k == kLightSamples - 1) sh->last_first = t;
+                    if (k == kLightSamples - 1) {
+                        sh->last_first = t;
+                        sh->leak = U.obj;
+                    }
                     sh->occ[k] = true;
                 }
             }
@@ -374,8 +382,7 @@ PT_HD D3 shadow_color(const SceneK& S, D3 n, int obj, const ShadowSet& sh, const
     }
     dsum /= (double)kLightSamples;
     const Mat& m = S.mat[obj];
-    // main.py:70: the object of the last ray's first occluder, else the last object
-    const Mat& lm = S.mat[sh.last_first < S.n_tri ? S.tri_obj[sh.last_first] : S.n_obj - 1];
+    const Mat& lm = S.mat[sh.leak];   // main.py:70
     bump<COUNT>(cnt, &Counters::shading_points, 1);
     return d3(m.rgb[0] * m.ka * S.ambient + S.light_rgb[0] * lm.rgb[0] * dsum,
               m.rgb[1] * m.ka * S.ambient + S.light_rgb[1] * lm.rgb[1] * dsum,

@@ -91,10 +91,11 @@ def _native_obj(path):
         import numpy as np
         from . import _native
         lib = _native.lib()
+        load = lib.pt_obj_load
     except Exception:
         return None
     m = C.POINTER(_native.PtMesh)()
-    if lib.pt_obj_load(path.encode(), C.byref(m)) != 0:
+    if load(path.encode(), C.byref(m)) != 0:
         return None
     try:
         M = m.contents

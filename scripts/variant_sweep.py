@@ -23,7 +23,7 @@ print("%%-40s split=%%s  kernel_ms min %%.3f med %%.3f  Mpath/s %%.1f  exact=%%s
 splits = os.environ.get("SPLITS", "auto").split(",")
 for lib in sys.argv[1:]:
     for sp in splits:
-        env = dict(os.environ, PT_HIP_LIB=os.path.abspath(lib))
+        env = dict(os.environ, PT_HIP_LIB=os.path.abspath(lib), PT_DEV_OLD_LIB="1")
         if sp != "auto":
             env["PT_SPLIT"] = sp
         r = subprocess.run([sys.executable, "-c", CHILD], env=env, timeout=300)
