@@ -128,7 +128,7 @@ struct SceneK {
     double center[3];
     const BNode* bnode;         // [n_bnode] BVH of the mesh objects' units (none: n_bnode = 0)
     const UnitF* bunit;         // [n_bunit] those units in leaf order
-    int32_t n_bnode, n_bunit, bvh_min_tri, pad2;   // bvh_min_tri: lowest triangle index in it
+    int32_t n_bnode, n_bunit, bvh_min_tri, bvh_min_obj;   // lowest triangle / object in it
 };
 
 // ------------------------------------------------------------------ RNG --

@@ -222,7 +222,12 @@ struct ShadowSet {
     float hlo[kLightSamples], hhi[kLightSamples];
     bool occ[kLightSamples];
     int first[kLightSamples];  // count mode: lowest occluding triangle (n_tri: none)
-    int last_first;            // lowest occluding triangle of the last ray (n_tri: none)
+    // the last ray's first occluder (main.py:70): only its object matters for
+    // the colour, and objects are contiguous in scene order, so outside count
+    // mode the lowest occluding OBJECT is tracked (n_obj: none) — an occluded
+    // ray then only looks at lower objects; count mode tracks the lowest
+    // triangle (n_tri: none) for the reference's test counts
+    int key2;
     int leak;                  // its object (main.py:70), the last object when none
 };
 
@@ -231,6 +236,7 @@ struct ShadowSet {
 // The points go to the spill; f32 copies of the directions and distance
 // brackets into sh.  `u` is either the 12 explicit uniforms (batched API) or
 // null, in which case block k of (pixel, sample, bounce) is drawn here.
+template <bool COUNT>
 PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, uint32_t pixel,
                         uint32_t sample, uint32_t bounce_i, ShadowSet* sh, const Spill& sp) {
 #pragma unroll
@@ -254,7 +260,7 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, u
         sh->occ[k] = false;
         sh->first[k] = S.n_tri;
     }
-    sh->last_first = S.n_tri;
+    sh->key2 = COUNT ? S.n_tri : S.n_obj;
     sh->leak = S.n_obj - 1;
 }
 
@@ -269,7 +275,9 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, u
 template <bool FORCE64, bool COUNT>
 PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
                       bool do_shadow, bool do_closest, ShadowSet* sh, F3 n32, ClosestAcc* ca,
-                      const Spill& sp, Counters* cnt) {
+                      const Spill& sp, Counters* cnt, uint32_t rays = 15u) {
+    // rays: bit k = shadow ray k, bit 3 = the closest ray (the BVH passes the
+    // lines that reached the leaf's box; a line that did not cannot hit)
     uint32_t amb = 0;   // bit 2k+i: shadow ray k / triangle i; bit 6+i: closest / triangle i
     const bool two = (U.count == 2);
     bool occ0[kLightSamples];
@@ -278,6 +286,7 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
     if (do_shadow) {
 #pragma unroll
         for (int k = 0; k < kLightSamples; ++k) {
+            if (!((rays >> k) & 1u)) continue;
             bool c0 = false, c1 = false, a0 = true, a1 = two;
             if (!FORCE64) {
                 const RayPlane p = ray_plane(U, O.h, sh->d32[k], sh->hlo[k], sh->hhi[k]);
@@ -296,20 +305,20 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
             // its lowest occluder is known (the leaked colour).  Units may come
             // in any order (the BVH), so "first" is the lowest triangle index.
             const int t0 = U.tri[0].t;
-            const bool need = (k == kLightSamples - 1) ? (t0 < sh->last_first)
+            const bool need = (k == kLightSamples - 1) ? ((COUNT ? t0 : U.obj) < sh->key2)
                               : (COUNT ? (t0 < sh->first[k]) : !occ0[k]);
             const bool c = c0 | c1;
             const int tc = c0 ? t0 : U.tri[1].t;
             if (COUNT && c && tc < sh->first[k]) sh->first[k] = tc;
-            if (k == kLightSamples - 1 && c && tc < sh->last_first) {
-                sh->last_first = tc;
+            if (k == kLightSamples - 1 && c && (COUNT ? tc : U.obj) < sh->key2) {
+                sh->key2 = COUNT ? tc : U.obj;
                 sh->leak = U.obj;
             }
             sh->occ[k] = occ0[k] | c;
             if (need) amb |= (a0 ? 1u : 0u) << (2 * k) | (a1 ? 2u : 0u) << (2 * k);
         }
     }
-    if (!FORCE64 && do_closest) {
+    if (!FORCE64 && do_closest && (rays & 8u)) {
         const RayPlane p = ray_plane(U, O.h, n32, INFINITY, INFINITY);
         const Verdict v0 = classify_tri(U.tri[0], p, O.bo0, O.co0, n32);
         bool c0 = v0.cand & !coplanar, c1 = false, a1 = false;
@@ -333,7 +342,7 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
                 if (!((amb >> (2 * k + i)) & 1u)) continue;
                 const int t = U.tri[i].t;
                 // decided meanwhile (a lower occluder of this unit, or occlusion)?
-                if (k == kLightSamples - 1 ? (t >= sh->last_first)
+                if (k == kLightSamples - 1 ? ((COUNT ? t : U.obj) >= sh->key2)
                                            : (COUNT ? (t >= sh->first[k]) : sh->occ[k]))
                     continue;
                 D3 Q;
@@ -344,7 +353,7 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
                     sqd < squared_dist(P, L)) {
                     if (COUNT && t < sh->first[k]) sh->first[k] = t;
                     if (k == kLightSamples - 1) {
-                        sh->last_first = t;
+                        sh->key2 = COUNT ? t : U.obj;
                         sh->leak = U.obj;
                     }
                     sh->occ[k] = true;
@@ -407,28 +416,32 @@ PT_HD void bvh_pass(const SceneK& S, F3 o32, int ogrp, bool do_shadow, bool do_c
     int node = (do_shadow || do_closest) ? 0 : -1;
     while (node >= 0) {
         int leaf = -1;
+        uint32_t leaf_rays = 0;
         while (node >= 0) {
             const BNode N = S.bnode[node];
             const F3 l = {N.lo[0] - o32.x, N.lo[1] - o32.y, N.lo[2] - o32.z};
             const F3 h = {N.hi[0] - o32.x, N.hi[1] - o32.y, N.hi[2] - o32.z};
-            bool hit = false;
+            uint32_t rays = 0;
             if (do_shadow) {
 #pragma unroll
                 for (int k = 0; k < kLightSamples; ++k) {
                     // rays still open: 0, 1 until occluded (count mode: until no BVH
-                    // triangle can be their lowest occluder); the last ray likewise
-                    const bool open = (k == kLightSamples - 1) ? (sh->last_first > S.bvh_min_tri)
+                    // triangle can be their lowest occluder); the last ray until
+                    // no BVH object can be its first occluder's
+                    const bool open = (k == kLightSamples - 1)
+                                          ? (sh->key2 > (COUNT ? S.bvh_min_tri : S.bvh_min_obj))
                                       : (COUNT ? (sh->first[k] > S.bvh_min_tri) : !sh->occ[k]);
-                    hit |= open && box_hit(l, h, inv[k], sh->hhi[k]);
+                    if (open && box_hit(l, h, inv[k], sh->hhi[k])) rays |= 1u << k;
                 }
             }
-            if (do_closest) hit |= box_hit(l, h, invc, ca->b1);
-            if (hit && N.leaf >= 0) {
+            if (do_closest && box_hit(l, h, invc, ca->b1)) rays |= 8u;
+            if (rays && N.leaf >= 0) {
                 leaf = N.leaf;
+                leaf_rays = rays;
                 node = N.skip;
                 break;
             }
-            node = hit ? node + 1 : N.skip;
+            node = rays ? node + 1 : N.skip;
         }
         if (leaf >= 0) {
             const int u0 = leaf >> 3, nu = leaf & 7;
@@ -436,7 +449,7 @@ PT_HD void bvh_pass(const SceneK& S, F3 o32, int ogrp, bool do_shadow, bool do_c
                 const UnitF U = S.bunit[u0 + i];
                 const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
                 fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, do_shadow, do_closest, sh, n32,
-                                           ca, sp, cnt);
+                                           ca, sp, cnt, leaf_rays);
             }
         }
     }
@@ -474,7 +487,7 @@ PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
              const Spill& sp, Counters* cnt) {
     ShadowSet sh;
     sp.put3(kSpP, P);
-    shadow_setup(S, P, u, 0, 0, 0, 0, &sh, sp);
+    shadow_setup<COUNT>(S, P, u, 0, 0, 0, 0, &sh, sp);
     const F3 o32 = to_f3(P - ld3(S.center));
     for (int u = 0; u < S.n_obj_unit; ++u) {
         if (PT_WAVE_ALL(sh.occ[0] && sh.occ[1] && sh.occ[2])) break;
@@ -594,7 +607,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         ShadowSet sh;
         sp.put3(kSpP, P);
         sp.put3(kSpNd, nd);
-        shadow_setup(S, P, nullptr, J.seed, J.pixel, sample, (uint32_t)b, &sh, sp);
+        shadow_setup<COUNT>(S, P, nullptr, J.seed, J.pixel, sample, (uint32_t)b, &sh, sp);
         const F3 o32 = to_f3(P - ld3(S.center));
         const F3 n32 = to_f3(unit(nd));
         ClosestAcc ca = closest_init();

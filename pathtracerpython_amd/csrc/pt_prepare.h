@@ -158,6 +158,7 @@ inline void build_bvh(HostScene* H, double X) {
     K.n_bnode = 0;
     K.n_bunit = (int32_t)H->bunit.size();
     K.bvh_min_tri = K.n_tri;
+    K.bvh_min_obj = K.n_obj;
     const int n = (int)H->bunit.size();
     if (n == 0) return;
     BvhBuilder B;
@@ -171,6 +172,7 @@ inline void build_bvh(HostScene* H, double X) {
         for (int m = 0; m < U.count; ++m) {
             const TriD& T = H->trid[U.tri[m].t];
             K.bvh_min_tri = std::min(K.bvh_min_tri, U.tri[m].t);
+            K.bvh_min_obj = std::min(K.bvh_min_obj, U.obj);
             const double* vs[3] = {T.v1, T.v2, T.v3};
             for (int v = 0; v < 3; ++v)
                 for (int a = 0; a < 3; ++a) {

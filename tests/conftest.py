@@ -58,14 +58,14 @@ def hostcheck():
     return lib
 
 
-def hc_render(lib, packed, params, force64=False):
+def hc_render(lib, packed, params, force64=False, count=True):
     from pathtracerpython_amd._abi import band_rows
     rows = len(band_rows(params.height, params.row_begin, params.row_end, params.row_step,
                          params.row_phase))
     out = np.zeros((rows, params.width, 3), dtype=np.float64)
     cnt = (C.c_uint64 * 8)()
     rc = lib.hc_render(C.byref(packed.desc), C.byref(params), int(force64),
-                       out.ctypes.data_as(C.POINTER(C.c_double)), cnt)
+                       out.ctypes.data_as(C.POINTER(C.c_double)), cnt if count else None)
     assert rc == 0
     names = ("closest_tests", "shadow_tests", "ray_bounces", "shading_points", "light_hits",
              "escapes", "f64_fallbacks", "f64_rescans")

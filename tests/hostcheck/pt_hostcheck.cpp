@@ -49,12 +49,16 @@ int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
             D3 P0 = d3(0, 0, 0);
             int tri0 = -1;
             D3 acc;
+            // counters requested: the count-mode lane code (exact first
+            // occluders); else the render kernel's own (object-level) one
             if (force64) {
                 if (p->bounces > 0) tri0 = closest<true, false>(H.k, eye, d0, -1, sp, &P0, &c);
-                acc = render_lane<true, true>(H.k, J, d0, tri0, P0, sp, &c);
+                acc = counters ? render_lane<true, true>(H.k, J, d0, tri0, P0, sp, &c)
+                               : render_lane<true, false>(H.k, J, d0, tri0, P0, sp, &c);
             } else {
                 if (p->bounces > 0) tri0 = closest<false, false>(H.k, eye, d0, -1, sp, &P0, &c);
-                acc = render_lane<false, true>(H.k, J, d0, tri0, P0, sp, &c);
+                acc = counters ? render_lane<false, true>(H.k, J, d0, tri0, P0, sp, &c)
+                               : render_lane<false, false>(H.k, J, d0, tri0, P0, sp, &c);
             }
             double* o = out + ((size_t)(rows - 1 - r) * p->width + ix) * 3;
             o[0] = acc.x / p->spp; o[1] = acc.y / p->spp; o[2] = acc.z / p->spp;

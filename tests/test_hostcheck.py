@@ -41,6 +41,8 @@ def test_kernel_code_matches_reference(hostcheck, packed, name, g, force64):
     W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
     fb, st = hc_render(hostcheck, packed, make_params(W, H, spp, B, seed), force64)
     assert np.abs(to_list_order(fb) - g["colors"]).max() <= 1e-12
+    fb2, _ = hc_render(hostcheck, packed, make_params(W, H, spp, B, seed), force64, count=False)
+    assert np.array_equal(fb2, fb)   # the render kernel's non-count lane code
     _, ost = oracle.render(packed, W, H, spp, B, seed)
     for k in ("closest_tests", "shadow_tests", "ray_bounces", "shading_points", "light_hits",
               "escapes"):
@@ -113,6 +115,10 @@ def _bvh_case(hostcheck, pk, W, H, spp, B, seed, flags=0):
     for k in ("closest_tests", "shadow_tests", "ray_bounces", "shading_points", "light_hits",
               "escapes"):
         assert sa[k] == ost[k] == sb[k], k
+    # the render kernel's own (non-count) lane code: object-level first occluder
+    c, _ = hc_render(hostcheck, pk, p, False, count=False)
+    d, _ = hc_render(hostcheck, pk, p, True, count=False)
+    assert np.array_equal(c, a) and np.array_equal(d, a)
 
 
 @pytest.mark.parametrize("n_tris,seed", [(64, 5), (300, 21), (1500, 22)])
