@@ -129,6 +129,7 @@ struct SceneK {
     const BNode* bnode;         // [n_bnode] BVH of the mesh objects' units (none: n_bnode = 0)
     const UnitF* bunit;         // [n_bunit] those units in leaf order
     int32_t n_bnode, n_bunit, bvh_min_tri, bvh_min_obj;   // lowest triangle / object in it
+    int32_t bvh_depth, pad3[3];  // levels below the root (the ordered traversal's stack need)
 };
 
 // ------------------------------------------------------------------ RNG --

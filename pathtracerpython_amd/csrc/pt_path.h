@@ -280,10 +280,10 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
     // lines that reached the leaf's box; a line that did not cannot hit)
     uint32_t amb = 0;   // bit 2k+i: shadow ray k / triangle i; bit 6+i: closest / triangle i
     const bool two = (U.count == 2);
-    bool occ0[kLightSamples];
+    if (do_shadow) {   // (sh is only touched here and for shadow bits: null without shadows)
+        bool occ0[kLightSamples];
 #pragma unroll
-    for (int k = 0; k < kLightSamples; ++k) occ0[k] = sh->occ[k];
-    if (do_shadow) {
+        for (int k = 0; k < kLightSamples; ++k) occ0[k] = sh->occ[k];
 #pragma unroll
         for (int k = 0; k < kLightSamples; ++k) {
             if (!((rays >> k) & 1u)) continue;
@@ -455,6 +455,62 @@ PT_HD void bvh_pass(const SceneK& S, F3 o32, int ogrp, bool do_shadow, bool do_c
     }
 }
 
+// The closest ray alone, nearest box first (by the smallest |t| of the line
+// inside it: the line is two-sided), with a per-lane stack of the farther
+// children; a popped node is dropped when its distance exceeds the bound the
+// candidates found meanwhile give (the best's upper |t|).
+constexpr int kBvhStack = 48;
+PT_HD float box_dist(F3 l, F3 h, F3 inv, float R) {   // INFINITY: not within |t| <= R
+    const float ax = l.x * inv.x, bx = h.x * inv.x;
+    const float ay = l.y * inv.y, by = h.y * inv.y;
+    const float az = l.z * inv.z, bz = h.z * inv.z;
+    const float tmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    const float d = tmin > 0.0f ? tmin : (tmax < 0.0f ? -tmax : 0.0f);
+    return ((tmin <= tmax) & (tmin <= R) & (tmax >= -R)) ? d : INFINITY;
+}
+PT_HD float node_dist(const SceneK& S, int i, F3 o32, F3 inv, float R) {
+    const BNode N = S.bnode[i];
+    const F3 l = {N.lo[0] - o32.x, N.lo[1] - o32.y, N.lo[2] - o32.z};
+    const F3 h = {N.hi[0] - o32.x, N.hi[1] - o32.y, N.hi[2] - o32.z};
+    return box_dist(l, h, inv, R);
+}
+template <bool COUNT>
+PT_HD void bvh_closest(const SceneK& S, F3 o32, int ogrp, F3 d32, ClosestAcc* ca, const Spill& sp,
+                       Counters* cnt) {
+    const F3 inv = rcp_dir(d32);
+    int stack[kBvhStack];
+    float sdist[kBvhStack];
+    int top = 0;
+    int node = node_dist(S, 0, o32, inv, ca->b1) < INFINITY ? 0 : -1;
+    while (node >= 0) {
+        const BNode N = S.bnode[node];
+        int next = -1;
+        if (N.leaf >= 0) {
+            const int u0 = N.leaf >> 3, nu = N.leaf & 7;
+            for (int i = 0; i < nu; ++i) {
+                const UnitF U = S.bunit[u0 + i];
+                fused_unit<false, COUNT>(S, U, origin_u(U, o32), U.grp == ogrp, false, true,
+                                         nullptr, d32, ca, sp, cnt, 8u);
+            }
+        } else {
+            const int a = node + 1, b = S.bnode[a].skip;   // left child, right child
+            const float da = node_dist(S, a, o32, inv, ca->b1);
+            const float db = node_dist(S, b, o32, inv, ca->b1);
+            const bool near_a = da <= db;
+            const int n0 = near_a ? a : b, n1 = near_a ? b : a;
+            const float d0 = near_a ? da : db, d1 = near_a ? db : da;
+            if (d1 < INFINITY) { stack[top] = n1; sdist[top] = d1; ++top; }
+            if (d0 < INFINITY) next = n0;
+        }
+        while (next < 0 && top > 0) {   // pop, dropping nodes beyond the current bound
+            --top;
+            if (sdist[top] <= ca->b1) next = stack[top];
+        }
+        node = next;
+    }
+}
+
 // Standalone query (primary rays, the batched intersect_objects API).  d need
 // not be normalised (utils.py:110).  ogrp: coplanar group of the triangle the
 // origin lies on (-1: none).
@@ -474,8 +530,12 @@ PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, const Spill& sp, D3* P,
                                 &acc, cnt);
         }
         if (BVH && S.n_bnode) {   // the meshes: closest ray only
-            ShadowSet none = {};
-            bvh_pass<false, COUNT>(S, o32, ogrp, false, true, &none, d32, &acc, sp, cnt);
+            if (S.bvh_depth < kBvhStack) {
+                bvh_closest<COUNT>(S, o32, ogrp, d32, &acc, sp, cnt);
+            } else {
+                ShadowSet none = {};
+                bvh_pass<false, COUNT>(S, o32, ogrp, false, true, &none, d32, &acc, sp, cnt);
+            }
         }
     }
     return closest_finish<FORCE64, COUNT, BVH>(S, acc, o, dn, P, cnt);
@@ -619,8 +679,12 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
             fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
                                        &ca, sp, cnt);
         }
-        if (BVH && S.n_bnode)   // the meshes
-            bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, !FORCE64 && trace, &sh, n32, &ca, sp, cnt);
+        if (BVH && S.n_bnode) {   // the meshes: shadows as a packet, the closest ray ordered
+            const bool ordered = S.bvh_depth < kBvhStack;
+            bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, !FORCE64 && trace && !ordered, &sh, n32,
+                                     &ca, sp, cnt);
+            if (!FORCE64 && trace && ordered) bvh_closest<COUNT>(S, o32, ogrp, n32, &ca, sp, cnt);
+        }
         if (!FORCE64 && any_trace) {
             for (int u = S.n_obj_unit; u < S.n_unit; ++u) {   // the light's units
                 const UnitF U = S.unit[u];

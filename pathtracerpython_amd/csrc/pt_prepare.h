@@ -124,7 +124,9 @@ struct BvhBuilder {
         if (mid <= b || mid >= e) mid = (b + e) / 2;   // coincident centroids: halve
         return mid;
     }
-    int build(int b, int e) {   // returns the subtree's root node
+    int depth = 0;
+    int build(int b, int e, int level = 0) {   // returns the subtree's root node
+        depth = std::max(depth, level);
         BNode N{};
         double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (int i = b; i < e; ++i)
@@ -144,8 +146,8 @@ struct BvhBuilder {
             H->bnode[node].leaf = ((int32_t)ordered.size() << 3) | (e - b);
             for (int i = b; i < e; ++i) ordered.push_back(H->bunit[idx[i]]);
         } else {
-            build(b, mid);
-            build(mid, e);
+            build(b, mid, level + 1);
+            build(mid, e, level + 1);
         }
         H->bnode[node].skip = (int)H->bnode.size();   // the node after this subtree
         return node;
@@ -159,6 +161,7 @@ inline void build_bvh(HostScene* H, double X) {
     K.n_bunit = (int32_t)H->bunit.size();
     K.bvh_min_tri = K.n_tri;
     K.bvh_min_obj = K.n_obj;
+    K.bvh_depth = 0;
     const int n = (int)H->bunit.size();
     if (n == 0) return;
     BvhBuilder B;
@@ -191,6 +194,7 @@ inline void build_bvh(HostScene* H, double X) {
         if (N.skip >= total) N.skip = -1;
     H->bunit.swap(B.ordered);
     K.n_bnode = total;
+    K.bvh_depth = B.depth;
 }
 
 inline D3 tri_vertex(const pt_scene_desc* d, int t, int v) {
