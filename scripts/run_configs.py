@@ -1,0 +1,90 @@
+"""Run BASELINE.json's single-GPU configurations at their full sizes on one
+MI355X and record kernel time, throughput and parity checks (dev tool; the
+bench line is bench.py's K2).  Writes one JSON object per line to stdout.
+
+  K1  64x64, 1 spp, 1 bounce        whole image vs the CPU oracle, hybrid == forced-f64
+  K2  512x512, 64 spp, 4 bounces    = bench.py's workload; oracle on 4 rows
+  K3  1024x1024, 1024 spp, 8 b + RR oracle on 2 rows (all 1024 spp)
+  K5  100k-triangle mesh, 1024x1024, 256 spp, 4 b   oracle on 64 pixels
+K4 (4096^2 x 4096 spp over 8 GPUs) is the driver's multi-GPU run of bench.py.
+Usage: run_configs.py [K1,K2,K3,K5]"""
+import json, os, sys, tempfile, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np
+import torch
+from oracle import oracle
+from pathtracerpython_amd import scene_reader
+from pathtracerpython_amd.render import Renderer
+from pathtracerpython_amd.synth import write_k5_scene
+
+scene_reader.VERBOSE = False
+CORNELL = os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl")
+only = sys.argv[1].split(",") if len(sys.argv) > 1 else ["K1", "K2", "K3", "K5"]
+
+
+def timed(r, W, H, spp, B, rr=False, reps=2):
+    p = r.params(W, H, spp, B, 9, rr=rr, out_f64=True)
+    fb = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    ms = []
+    for _ in range(reps):
+        r.render_device(p, fb.data_ptr(), s)
+        torch.cuda.synchronize()
+        ms.append(r.last_kernel_ms())
+    return fb.cpu().numpy(), min(ms)
+
+
+def check_pixels(r, fb, W, H, spp, B, pix, rr=False):
+    from pathtracerpython_amd._abi import PT_FLAG_RR
+    t0 = time.time()
+    cols, _ = oracle.render(r.packed, W, H, spp, B, 9, flags=PT_FLAG_RR if rr else 0,
+                            pixels=np.asarray(pix, dtype=np.int64), threads=16)
+    got = np.array([fb[H - 1 - (k % H), k // H] for k in pix])
+    return float(np.abs(got - cols).max()), time.time() - t0
+
+
+def emit(name, W, H, spp, B, rr, ms, linf, n_checked, extra=None):
+    d = {"config": name, "width": W, "height": H, "spp": spp, "bounces": B, "rr": rr,
+         "kernel_ms": round(ms, 3), "Mpath_per_s": round(W * H * spp / ms / 1e3, 2),
+         "linf_vs_oracle_f64": linf, "oracle_pixels": n_checked}
+    d.update(extra or {})
+    print(json.dumps(d), flush=True)
+
+
+with Renderer(scene_reader.Scene(CORNELL)) as r:
+    if "K1" in only:
+        W = H = 64
+        fb, ms = timed(r, W, H, 1, 1)
+        f64 = r.render(W, H, 1, 1, 9, out_f64=True, force_f64=True)
+        linf, _ = check_pixels(r, fb, W, H, 1, 1, range(W * H))
+        emit("K1", W, H, 1, 1, False, ms, linf, W * H, {"bitwise_eq_forced_f64": bool(np.array_equal(fb, f64))})
+    if "K2" in only:
+        W = H = 512
+        fb, ms = timed(r, W, H, 64, 4)
+        rows = [0, 131, 262, 511]
+        linf, _ = check_pixels(r, fb, W, H, 64, 4, [ix * H + iy for iy in rows for ix in range(W)])
+        emit("K2", W, H, 64, 4, False, ms, linf, 4 * W)
+    if "K3" in only:
+        W = H = 1024
+        fb, ms = timed(r, W, H, 1024, 8, rr=True, reps=1)
+        rows = [300, 700]
+        pix = [ix * H + iy for iy in rows for ix in range(0, W, 8)]
+        linf, sec = check_pixels(r, fb, W, H, 1024, 8, pix, rr=True)
+        emit("K3", W, H, 1024, 8, True, ms, linf, len(pix), {"oracle_s": round(sec, 1)})
+if "K5" in only:
+    sdl = write_k5_scene(tempfile.mkdtemp(), n_tris=100_000, seed=0, size=1024)
+    t0 = time.time()
+    with Renderer(scene_reader.Scene(sdl)) as r:
+        setup = time.time() - t0
+        W = H = 1024
+        fb, ms = timed(r, W, H, 256, 4, reps=1)
+        rs = np.random.RandomState(0)
+        pix = sorted(rs.choice(W * H, 64, replace=False).tolist())
+        linf, sec = check_pixels(r, fb, W, H, 256, 4, pix)
+        small = r.render(64, 64, 2, 4, 9, out_f64=True)
+        small64 = r.render(64, 64, 2, 4, 9, out_f64=True, force_f64=True)
+        emit("K5", W, H, 256, 4, False, ms, linf, len(pix),
+             {"triangles": int(r.packed.n_tri), "ingest_bvh_upload_s": round(setup, 2),
+              "oracle_s": round(sec, 1),
+              "bitwise_eq_forced_f64_64x64x2": bool(np.array_equal(small, small64))})
