@@ -414,11 +414,17 @@ PT_HD void bvh_pass(const SceneK& S, F3 o32, int ogrp, bool do_shadow, bool do_c
     // "while-while": each lane walks internal nodes on its own until it finds
     // a leaf its lines reach, then the lanes test their leaves together
     int node = (do_shadow || do_closest) ? 0 : -1;
+    BNode N = S.bnode[0];
     while (node >= 0) {
         int leaf = -1;
         uint32_t leaf_rays = 0;
         while (node >= 0) {
-            const BNode N = S.bnode[node];
+            // both possible successors are fetched while this node is tested,
+            // so the walk waits on one load per step, overlapped with the test
+            const int na = node + 1 < S.n_bnode ? node + 1 : node;
+            const int nb = N.skip >= 0 ? N.skip : node;
+            const BNode A = S.bnode[na];
+            const BNode B = S.bnode[nb];
             const F3 l = {N.lo[0] - o32.x, N.lo[1] - o32.y, N.lo[2] - o32.z};
             const F3 h = {N.hi[0] - o32.x, N.hi[1] - o32.y, N.hi[2] - o32.z};
             uint32_t rays = 0;
@@ -439,9 +445,12 @@ PT_HD void bvh_pass(const SceneK& S, F3 o32, int ogrp, bool do_shadow, bool do_c
                 leaf = N.leaf;
                 leaf_rays = rays;
                 node = N.skip;
+                N = B;
                 break;
             }
-            node = rays ? node + 1 : N.skip;
+            const bool down = rays != 0;   // (a leaf's skip is node + 1: A == B)
+            node = down ? node + 1 : N.skip;
+            N = down ? A : B;
         }
         if (leaf >= 0) {
             const int u0 = leaf >> 3, nu = leaf & 7;
