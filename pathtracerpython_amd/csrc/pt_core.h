@@ -156,6 +156,33 @@ PT_HD void rng_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bo
     philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
+// The 4 blocks of one (pixel, sample, bounce) — slots 0..15 — in lockstep:
+// four independent 10-round chains interleaved, instead of one chain at a time
+PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce,
+                       uint32_t w[16]) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        w[4 * b] = pixel; w[4 * b + 1] = sample; w[4 * b + 2] = bounce; w[4 * b + 3] = (uint32_t)b;
+    }
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            uint32_t* c = w + 4 * b;
+            const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+            const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+            const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+            const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+            c[1] = (uint32_t)p1;
+            c[3] = (uint32_t)p0;
+            c[0] = n0;
+            c[2] = n2;
+        }
+    }
+}
+
 PT_HD double u_of(uint32_t w) { return (double)(w >> 8) * (1.0 / 16777216.0); }
 
 // ------------------------------------------------------------- vectors --

@@ -228,6 +228,7 @@ struct ShadowSet {
     // ray then only looks at lower objects; count mode tracks the lowest
     // triangle (n_tri: none) for the reference's test counts
     int key2;
+    double ln[kLightSamples];  // l_k . n of each light sample (main.py:66-68), from setup
     int leak;                  // its object (main.py:70), the last object when none
 };
 
@@ -237,8 +238,9 @@ struct ShadowSet {
 // brackets into sh.  `u` is either the 12 explicit uniforms (batched API) or
 // null, in which case block k of (pixel, sample, bounce) is drawn here.
 template <bool COUNT>
-PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, uint32_t pixel,
-                        uint32_t sample, uint32_t bounce_i, ShadowSet* sh, const Spill& sp) {
+PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double* u, uint64_t seed,
+                        uint32_t pixel, uint32_t sample, uint32_t bounce_i, ShadowSet* sh,
+                        const Spill& sp) {
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
         double u0, u1, u2, u3;
@@ -257,6 +259,7 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, const double* u, uint64_t seed, u
         sh->hlo[k] = tl * (1.0f - 1e-6f);
         sh->hhi[k] = tl * (1.0f + 1e-6f);
         sh->d32[k] = to_f3(dn);
+        sh->ln[k] = dot(dn, n);
         sh->occ[k] = false;
         sh->first[k] = S.n_tri;
     }
@@ -378,13 +381,11 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
 }
 
 template <bool COUNT>
-PT_HD D3 shadow_color(const SceneK& S, D3 n, int obj, const ShadowSet& sh, const Spill& sp,
-                      Counters* cnt) {
+PT_HD D3 shadow_color(const SceneK& S, int obj, const ShadowSet& sh, Counters* cnt) {
     double dsum = 0.0;
-    const D3 P = sp.get3(kSpP);
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
-        if (!sh.occ[k]) dsum += dot(unit(sp.get3(kSpL + 3 * k) - P), n);   // main.py:66-68
+        if (!sh.occ[k]) dsum += sh.ln[k];   // main.py:66-68
         // the reference's loop stops at the first occluder (main.py:42-55)
         bump<COUNT>(cnt, &Counters::shadow_tests,
                     (uint32_t)(sh.first[k] < S.n_tri ? sh.first[k] + 1 : S.n_obj_tri));
@@ -556,7 +557,7 @@ PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
              const Spill& sp, Counters* cnt) {
     ShadowSet sh;
     sp.put3(kSpP, P);
-    shadow_setup<COUNT>(S, P, u, 0, 0, 0, 0, &sh, sp);
+    shadow_setup<COUNT>(S, P, n, u, 0, 0, 0, 0, &sh, sp);
     const F3 o32 = to_f3(P - ld3(S.center));
     for (int u = 0; u < S.n_obj_unit; ++u) {
         if (PT_WAVE_ALL(sh.occ[0] && sh.occ[1] && sh.occ[2])) break;
@@ -567,7 +568,7 @@ PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
     }
     if (BVH && S.n_bnode)
         bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, false, &sh, F3{0.f, 0.f, 0.f}, nullptr, sp, cnt);
-    return shadow_color<COUNT>(S, n, obj, sh, sp, cnt);
+    return shadow_color<COUNT>(S, obj, sh, cnt);
 }
 
 // ---------------------------------------------------------------- bounce --
@@ -656,27 +657,33 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         const TriS R = S.tris[tri];
         const Mat& m = S.mat[obj];
         const int ogrp = S.tri_grp[tri];
-        // RNG: slots 12..15 (block 3) bounce + RR here; slots 0..11 (blocks
-        // 0..2) light sampling, drawn in shadow_setup
-        uint32_t w[4];
-        rng_block(J.seed, J.pixel, sample, (uint32_t)b, 3u, w);
-        // next ray first (main.py:236-268): it does not depend on the colour
+        // RNG: the 16 slots of this bounce (4 Philox blocks in lockstep):
+        // 0..11 light sampling, 12..14 the bounce, 15 Russian roulette
+        uint32_t w[16];
+        rng_blocks4(J.seed, J.pixel, sample, (uint32_t)b, w);
+        ShadowSet sh;
+        {
+            double u12[12];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) u12[i] = u_of(w[i]);
+            shadow_setup<COUNT>(S, P, ld3(R.n), u12, 0, 0, 0, 0, &sh, sp);
+        }
+        // next ray (main.py:236-268): it does not depend on the colour
         double kf;
-        const D3 nd = bounce(S, R, m, P, sp.get3(kSpNd), u_of(w[0]), u_of(w[1]), u_of(w[2]), &kf);
+        const D3 nd = bounce(S, R, m, P, sp.get3(kSpNd), u_of(w[12]), u_of(w[13]), u_of(w[14]),
+                             &kf);
         const double kn = k * kf;
         bool trace = (b + 1 < J.bounces);
         double kk = kn;
         if (trace && J.rr_depth >= 0 && b >= J.rr_depth) {   // build extension
             double q = fabs(kn);
             q = q < 0.05 ? 0.05 : (q > 1.0 ? 1.0 : q);
-            if (u_of(w[3]) >= q) trace = false;
+            if (u_of(w[15]) >= q) trace = false;
             else kk = kn / q;
         }
         // one pass: 3 shadow rays + the next ray's closest hit, same origin
-        ShadowSet sh;
         sp.put3(kSpP, P);
         sp.put3(kSpNd, nd);
-        shadow_setup<COUNT>(S, P, nullptr, J.seed, J.pixel, sample, (uint32_t)b, &sh, sp);
         const F3 o32 = to_f3(P - ld3(S.center));
         const F3 n32 = to_f3(unit(nd));
         ClosestAcc ca = closest_init();
@@ -701,8 +708,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
                                     &ca, cnt);
             }
         }
-        // the normal is re-read rather than kept live across the unit loop
-        const D3 col = shadow_color<COUNT>(S, ld3(S.tris[tri].n), obj, sh, sp, cnt);
+        const D3 col = shadow_color<COUNT>(S, obj, sh, cnt);
         acc = acc + col * k;   // main.py:230-231 (k before this bounce's update)
         k = kk;
         bool done = !trace;
