@@ -135,27 +135,6 @@ struct SceneK {
 // ------------------------------------------------------------------ RNG --
 // Philox4x32-10 (Salmon et al., SC'11), key = seed, counter =
 // (pixel, sample, bounce, slot>>2); see tests/golden/philox_ref.py.
-PT_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-        c[1] = (uint32_t)p1;
-        c[3] = (uint32_t)p0;
-        c[0] = n0;
-        c[2] = n2;
-    }
-}
-
-PT_HD void rng_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce,
-                     uint32_t blk, uint32_t w[4]) {
-    w[0] = pixel; w[1] = sample; w[2] = bounce; w[3] = blk;
-    philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
-}
-
 // The 4 blocks of one (pixel, sample, bounce) — slots 0..15 — in lockstep:
 // four independent 10-round chains interleaved, instead of one chain at a time
 PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce,

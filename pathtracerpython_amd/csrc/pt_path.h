@@ -235,22 +235,14 @@ struct ShadowSet {
 // Light sample k uses the uniforms of slots 4k..4k+3 (one Philox block: the
 // triangle pick utils.py:30 and the three barycentric draws utils.py:23).
 // The points go to the spill; f32 copies of the directions and distance
-// brackets into sh.  `u` is either the 12 explicit uniforms (batched API) or
-// null, in which case block k of (pixel, sample, bounce) is drawn here.
+// brackets into sh, with l_k . n for the colour.  u: the 12 uniforms (the
+// render loop draws them with rng_blocks4; the batched API passes them in).
 template <bool COUNT>
-PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double* u, uint64_t seed,
-                        uint32_t pixel, uint32_t sample, uint32_t bounce_i, ShadowSet* sh,
+PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double u[12], ShadowSet* sh,
                         const Spill& sp) {
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
-        double u0, u1, u2, u3;
-        if (u) {
-            u0 = u[4 * k]; u1 = u[4 * k + 1]; u2 = u[4 * k + 2]; u3 = u[4 * k + 3];
-        } else {
-            uint32_t w[4];
-            rng_block(seed, pixel, sample, bounce_i, (uint32_t)k, w);
-            u0 = u_of(w[0]); u1 = u_of(w[1]); u2 = u_of(w[2]); u3 = u_of(w[3]);
-        }
+        const double u0 = u[4 * k], u1 = u[4 * k + 1], u2 = u[4 * k + 2], u3 = u[4 * k + 3];
         const int li = pick_light(S, u0);
         const D3 L = light_point(S.trid[S.light_tri[li]], u1, u2, u3);
         sp.put3(kSpL + 3 * k, L);
@@ -557,7 +549,7 @@ PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
              const Spill& sp, Counters* cnt) {
     ShadowSet sh;
     sp.put3(kSpP, P);
-    shadow_setup<COUNT>(S, P, n, u, 0, 0, 0, 0, &sh, sp);
+    shadow_setup<COUNT>(S, P, n, u, &sh, sp);
     const F3 o32 = to_f3(P - ld3(S.center));
     for (int u = 0; u < S.n_obj_unit; ++u) {
         if (PT_WAVE_ALL(sh.occ[0] && sh.occ[1] && sh.occ[2])) break;
@@ -666,7 +658,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
             double u12[12];
 #pragma unroll
             for (int i = 0; i < 12; ++i) u12[i] = u_of(w[i]);
-            shadow_setup<COUNT>(S, P, ld3(R.n), u12, 0, 0, 0, 0, &sh, sp);
+            shadow_setup<COUNT>(S, P, ld3(R.n), u12, &sh, sp);
         }
         // next ray (main.py:236-268): it does not depend on the colour
         double kf;

@@ -231,4 +231,9 @@ int hc_bvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t*
     return 0;
 }
 
+// The kernel's RNG (rng_blocks4): the 16 words of one (pixel, sample, bounce).
+void hc_rng4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t* out) {
+    rng_blocks4(seed, pixel, sample, bounce, out);
+}
+
 }  // extern "C"

@@ -155,3 +155,20 @@ def test_filter_never_wrong_small_k5(hostcheck, tmp_path):
     out = (C.c_int64 * 4)()
     assert hostcheck.hc_bvh_check(C.byref(pk.desc), C.c_int64(100), C.c_uint64(4), out) == 0
     assert out[0] == 0 and out[1] == 0 and out[2] > 50
+
+
+@pytest.mark.parametrize("seed,pixel,sample,bounce", [(9, 0, 0, 0), (9, 262143, 63, 3),
+                                                      (0xDEADBEEFCAFE, 12345, 7, 7),
+                                                      (2**64 - 1, 2**32 - 1, 2**31, 1)])
+def test_kernel_rng_matches_reference_philox(hostcheck, seed, pixel, sample, bounce):
+    """rng_blocks4 (the kernel's 16 slots of a bounce) == the Philox4x32-10
+    keyed stream the goldens were made with (tests/golden/philox_ref.py)."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from philox_ref import philox4x32_10
+    out = (C.c_uint32 * 16)()
+    hostcheck.hc_rng4(C.c_uint64(seed), C.c_uint32(pixel), C.c_uint32(sample),
+                      C.c_uint32(bounce), out)
+    key = (seed & 0xFFFFFFFF, seed >> 32)
+    want = [w for blk in range(4) for w in philox4x32_10((pixel, sample, bounce, blk), key)]
+    assert list(out) == want
