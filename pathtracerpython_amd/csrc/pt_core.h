@@ -58,19 +58,21 @@ constexpr float kTzHi = 0.0031622809f;   // sqrt(1e-5) * (1 + 1e-6)
 //   grp    : coplanar group (host-verified in f64).  A line whose origin lies
 //            on a triangle of the same group meets this plane at |t| < 1e-4,
 //            i.e. squared distance < 1e-5: certainly not a usable hit.
-struct TriB {            // 12 words
+struct TriB {            // 8 words
     float gb[3], cb;
     float gc[3], cc;
-    float eo, ed, g;
-    int32_t t;           // triangle index in scene order
 };
-struct alignas(16) UnitF {   // 144 B: two s_load_dwordx16 + one dwordx4
+struct alignas(16) UnitF {   // 128 B: two s_load_dwordx16
     float n[3], cn;
     float eh, eq, qhi;
-    int32_t grp;
-    int32_t count, obj, pad1, pad2;   // obj: the members' object (one per unit)
+    float eo, ed, g;         // the members' barycentric bound (max over members)
+    int32_t grp, count;
+    int32_t obj;             // the members' object (one per unit)
+    int32_t t[2];            // member triangle indices in scene order
+    int32_t pad;
     TriB tri[2];
 };
+static_assert(sizeof(UnitF) == 128, "UnitF is two scalar x16 loads");
 
 // f64 exact record: the reference's plane normal and edges (utils.py:109-111,
 // :78-80).  cvp = dot(vp, v1).
@@ -231,6 +233,7 @@ enum : int { kMiss = 0, kCand = 1, kAmb = 2 };
 //   closest: valid iff sqd > 1e-5                 -> hi = inf
 //   shadow : occluder iff 1e-5 <= sqd < |L - P|^2 -> hi_lo/hi_hi bracket tL
 struct RayPlane {
+    float q;       // n . d
     float t, at, dt;
     float del;     // barycentric bound, shared by the unit's triangles (see classify_tri)
     bool rmiss;    // |t| certainly out of range: the test is a certain miss
@@ -239,14 +242,15 @@ struct RayPlane {
 PT_HD RayPlane ray_plane(const UnitF& U, float h, F3 d, float hi_lo, float hi_hi) {
     RayPlane p;
     const float q = lin3(U.n, d);
+    p.q = q;
     const float r = rcpf(q);
     p.t = -h * r;
     p.at = fabsf(p.t);
     // |t_ref - t| <= (eh + |t| eq) / |q|  (eq absorbs the 3u|t| of 1/q and t)
     p.dt = fabsf(r) * fmaf(p.at, U.eq, U.eh);
-    // the host stores the unit's bound coefficients (max over its triangles)
-    // in every member's eo/ed/g, so one del serves both triangles
-    p.del = fmaf(U.tri[0].g, p.dt, fmaf(p.at, U.tri[0].ed, U.tri[0].eo));
+    // the unit's bound coefficients are the max over its triangles, so one
+    // del serves both
+    p.del = fmaf(U.g, p.dt, fmaf(p.at, U.ed, U.eo));
     p.rmiss = (p.at + p.dt < kTzLo) | (p.at - p.dt >= hi_hi);
     p.rcand = (fabsf(q) > U.qhi) & (p.at - p.dt > kTzHi) & (p.at + p.dt < hi_lo);
     return p;

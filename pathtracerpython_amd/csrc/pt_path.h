@@ -85,7 +85,7 @@ PT_HD OriginU origin_u(const UnitF& U, F3 o) {
 }
 
 template <bool COUNT>
-PT_HD void closest_tri(const SceneK& S, const TriB& B, const RayPlane& p, float bo, float co,
+PT_HD void closest_tri(const SceneK& S, const TriB& B, int t, const RayPlane& p, float bo, float co,
                        F3 d32, bool coplanar, const Spill& sp, int o_slot, int dn_slot,
                        ClosestAcc* acc, Counters* cnt) {
     const int st = coplanar ? kMiss : verdict_code(classify_tri(B, p, bo, co, d32));
@@ -95,13 +95,13 @@ PT_HD void closest_tri(const SceneK& S, const TriB& B, const RayPlane& p, float 
         D3 Q;
         double sqd;
         bump<COUNT>(cnt, &Counters::fallbacks, 1);
-        if (eval64(S.trid[B.t], sp.get3(o_slot), unit(sp.get3(dn_slot)), &Q, &sqd) && sqd > kZero) {
+        if (eval64(S.trid[t], sp.get3(o_slot), unit(sp.get3(dn_slot)), &Q, &sqd) && sqd > kZero) {
             const float sq = sqrtf((float)sqd);   // |t| to ~1e-7; brackets are 1e-6
             a = sq * (1.0f - 1e-6f);
             b = sq * (1.0f + 1e-6f);
         }
     }
-    closest_add(acc, B.t, a, b);
+    closest_add(acc, t, a, b);
 }
 
 // One closest-hit ray against one plane unit.
@@ -110,9 +110,9 @@ PT_HD void closest_unit(const SceneK& S, const UnitF& U, const OriginU& O, F3 d3
                         const Spill& sp, int o_slot, int dn_slot, ClosestAcc* acc,
                         Counters* cnt) {
     const RayPlane p = ray_plane(U, O.h, d32, INFINITY, INFINITY);
-    closest_tri<COUNT>(S, U.tri[0], p, O.bo0, O.co0, d32, coplanar, sp, o_slot, dn_slot, acc, cnt);
+    closest_tri<COUNT>(S, U.tri[0], U.t[0], p, O.bo0, O.co0, d32, coplanar, sp, o_slot, dn_slot, acc, cnt);
     if (U.count == 2)
-        closest_tri<COUNT>(S, U.tri[1], p, O.bo1, O.co1, d32, coplanar, sp, o_slot, dn_slot, acc, cnt);
+        closest_tri<COUNT>(S, U.tri[1], U.t[1], p, O.bo1, O.co1, d32, coplanar, sp, o_slot, dn_slot, acc, cnt);
 }
 
 // BVH helpers (the traversal itself, bvh_pass, follows fused_unit below)
@@ -150,7 +150,7 @@ PT_HD void bvh_rescan(const SceneK& S, D3 o, D3 dn, float R, int* best, double* 
             for (int i = 0; i < nu; ++i) {
                 const UnitF& U = S.bunit[u0 + i];
                 for (int m = 0; m < U.count; ++m) {
-                    const int t = U.tri[m].t;
+                    const int t = U.t[m];
                     D3 Q;
                     double sqd;
                     if (eval64(S.trid[t], o, dn, &Q, &sqd) && sqd > kZero &&
@@ -190,7 +190,7 @@ PT_HD int closest_finish(const SceneK& S, const ClosestAcc& c, D3 o, D3 dn, D3* 
             for (int u = 0; u < S.n_unit; ++u) {
                 const UnitF& U = S.unit[u];
                 for (int m = 0; m < U.count; ++m) {
-                    const int t = U.tri[m].t;
+                    const int t = U.t[m];
                     D3 Q; double sqd;
                     if (eval64(S.trid[t], o, dn, &Q, &sqd) && sqd > kZero &&
                         (best < 0 || sqd < bsq || (sqd == bsq && t < best))) {
@@ -259,6 +259,73 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double u[12], ShadowS
     sh->leak = S.n_obj - 1;
 }
 
+// Shadow rays of the uniform (scene-order) loop with the filter verdicts as
+// float margins in VGPRs rather than lane masks: cand iff
+// min(cm, m - del) > 0, ambiguous iff min3(nm, m + del, -cand) >= 0 (cm, nm:
+// the plane part's candidate / not-miss margins), occlusion a running max
+// (> 0: occluded).  Same verdicts as classify_tri (boundary cases lean to
+// "ambiguous"), fewer SGPRs and scalar ops.  Render kernel only (not count
+// mode, not forced f64); ambiguous tests go to the same f64 block.
+#ifndef PT_MARGIN
+#define PT_MARGIN 1
+#endif
+// The candidate margins propagate NaN (v_minimum: a NaN compare is "not a
+// candidate" in classify_tri); the ambiguity margins drop it (fminf: a NaN
+// compare is "not certainly out").
+PT_HD float nan_min(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_elementwise_minimum(a, b);
+#else
+    return (a != a || b != b) ? NAN : fminf(a, b);
+#endif
+}
+// plane part: cm > 0 iff the range test is certain (rcand), nm >= 0 unless
+// it certainly fails (rmiss, boundary leaning to "not a miss"); cop = -1 for
+// a coplanar unit (certain miss), else +inf
+PT_HD void margin_plane(const UnitF& U, const RayPlane& p, float hi_lo, float hi_hi, float cop,
+                        float* cm, float* nm) {
+    const float lo = p.at - p.dt, hi = p.at + p.dt;
+    *cm = nan_min(nan_min(fabsf(p.q) - U.qhi, lo - kTzHi), nan_min(hi_lo - hi, cop));
+    *nm = fminf(fminf(hi - kTzLo, hi_hi - lo), cop);
+}
+PT_HD void margin_tri(const TriB& B, const RayPlane& p, float bo, float co, F3 d, float cm,
+                      float nm, float* c, float* a) {
+    const float beta = fmaf(p.t, lin3(B.gb, d), bo);
+    const float gam = fmaf(p.t, lin3(B.gc, d), co);
+    const float m = min3f(beta, gam, (1.0f - beta) - gam);
+    *c = nan_min(cm, m - p.del);
+    *a = fminf(fminf(nm, m + p.del), -*c);
+}
+PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
+                         ShadowSet* sh, float oc[kLightSamples], uint32_t* amb) {
+    const bool two = (U.count == 2);
+    const float cop = coplanar ? -1.0f : INFINITY;
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        const F3 d = sh->d32[k];
+        const RayPlane p = ray_plane(U, O.h, d, sh->hlo[k], sh->hhi[k]);
+        float cm, nm;
+        margin_plane(U, p, sh->hlo[k], sh->hhi[k], cop, &cm, &nm);
+        float c0, a0, c1 = -INFINITY, a1 = -INFINITY;
+        margin_tri(U.tri[0], p, O.bo0, O.co0, d, cm, nm, &c0, &a0);
+        if (two) margin_tri(U.tri[1], p, O.bo1, O.co1, d, cm, nm, &c1, &a1);   // wave-uniform
+        const float old = oc[k];
+        const float c = fmaxf(c0, c1);
+        oc[k] = fmaxf(old, c);
+        if (k == kLightSamples - 1) {
+            const bool need = U.obj < sh->key2;
+            if (c > 0.0f && need) {
+                sh->key2 = U.obj;
+                sh->leak = U.obj;
+            }
+            if (need) *amb |= (a0 >= 0.0f ? 1u : 0u) << (2 * k) | (a1 >= 0.0f ? 2u : 0u) << (2 * k);
+        } else {   // only while not occluded before this unit
+            *amb |= (fminf(a0, -old) >= 0.0f ? 1u : 0u) << (2 * k) |
+                    (fminf(a1, -old) >= 0.0f ? 2u : 0u) << (2 * k);
+        }
+    }
+}
+
 // One plane unit against the 3 shadow rays and the next ray's closest hit,
 // all from the same origin (the fused per-bounce pass).  Every verdict is
 // computed branch-free; ambiguous tests are only recorded as bits and
@@ -267,15 +334,18 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double u[12], ShadowS
 // each shadow ray the lowest occluding triangle index is tracked, so the
 // leaked colour of main.py:70 (object of the first occluder in scene order)
 // does not depend on the order units are visited in.
-template <bool FORCE64, bool COUNT>
+template <bool FORCE64, bool COUNT, bool MARGIN = false>
 PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
                       bool do_shadow, bool do_closest, ShadowSet* sh, F3 n32, ClosestAcc* ca,
-                      const Spill& sp, Counters* cnt, uint32_t rays = 15u) {
+                      const Spill& sp, Counters* cnt, uint32_t rays = 15u,
+                      float* oc = nullptr) {
     // rays: bit k = shadow ray k, bit 3 = the closest ray (the BVH passes the
     // lines that reached the leaf's box; a line that did not cannot hit)
     uint32_t amb = 0;   // bit 2k+i: shadow ray k / triangle i; bit 6+i: closest / triangle i
     const bool two = (U.count == 2);
-    if (do_shadow) {   // (sh is only touched here and for shadow bits: null without shadows)
+    if (MARGIN) {   // the render loop's uniform units (oc: occlusion margins)
+        if (do_shadow) shadow_unit_m(S, U, O, coplanar, sh, oc, &amb);
+    } else if (do_shadow) {   // (sh is only touched here and for shadow bits: null without shadows)
         bool occ0[kLightSamples];
 #pragma unroll
         for (int k = 0; k < kLightSamples; ++k) occ0[k] = sh->occ[k];
@@ -299,11 +369,11 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
             // mode: until their lowest occluder is known), the last ray until
             // its lowest occluder is known (the leaked colour).  Units may come
             // in any order (the BVH), so "first" is the lowest triangle index.
-            const int t0 = U.tri[0].t;
+            const int t0 = U.t[0];
             const bool need = (k == kLightSamples - 1) ? ((COUNT ? t0 : U.obj) < sh->key2)
                               : (COUNT ? (t0 < sh->first[k]) : !occ0[k]);
             const bool c = c0 | c1;
-            const int tc = c0 ? t0 : U.tri[1].t;
+            const int tc = c0 ? t0 : U.t[1];
             if (COUNT && c && tc < sh->first[k]) sh->first[k] = tc;
             if (k == kLightSamples - 1 && c && (COUNT ? tc : U.obj) < sh->key2) {
                 sh->key2 = COUNT ? tc : U.obj;
@@ -326,7 +396,7 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
         // both candidates of one unit cannot happen (a point certainly inside
         // one triangle is certainly outside its coplanar neighbour)
         const bool c = c0 | c1;
-        closest_add(ca, c0 ? U.tri[0].t : U.tri[1].t, c ? p.at - p.dt : INFINITY,
+        closest_add(ca, c0 ? U.t[0] : U.t[1], c ? p.at - p.dt : INFINITY,
                     c ? p.at + p.dt : INFINITY);
         amb |= (a0 ? 64u : 0u) | (a1 ? 128u : 0u);
     }
@@ -335,10 +405,11 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
         for (int k = 0; k < kLightSamples; ++k) {
             for (int i = 0; i < 2; ++i) {
                 if (!((amb >> (2 * k + i)) & 1u)) continue;
-                const int t = U.tri[i].t;
+                const int t = U.t[i];
                 // decided meanwhile (a lower occluder of this unit, or occlusion)?
                 if (k == kLightSamples - 1 ? ((COUNT ? t : U.obj) >= sh->key2)
-                                           : (COUNT ? (t >= sh->first[k]) : sh->occ[k]))
+                                           : (COUNT ? (t >= sh->first[k])
+                                                    : (MARGIN ? oc[k] > 0.0f : sh->occ[k])))
                     continue;
                 D3 Q;
                 double sqd;
@@ -351,13 +422,14 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
                         sh->key2 = COUNT ? t : U.obj;
                         sh->leak = U.obj;
                     }
-                    sh->occ[k] = true;
+                    if (MARGIN) oc[k] = 1.0f;
+                    else sh->occ[k] = true;
                 }
             }
         }
         for (int i = 0; i < 2; ++i) {
             if (!((amb >> (6 + i)) & 1u)) continue;
-            const int t = U.tri[i].t;
+            const int t = U.t[i];
             D3 Q;
             double sqd;
             bump<COUNT>(cnt, &Counters::fallbacks, 1);
@@ -680,12 +752,26 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         const F3 n32 = to_f3(unit(nd));
         ClosestAcc ca = closest_init();
         const bool any_trace = PT_WAVE_ANY(trace);
-        for (int u = 0; u < S.n_obj_unit; ++u) {
-            const UnitF U = S.unit[u];
-            const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
-            const bool do_shadow = PT_WAVE_ANY(!(sh.occ[0] && sh.occ[1] && sh.occ[2]));
-            fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
-                                       &ca, sp, cnt);
+        if (!FORCE64 && !COUNT && PT_MARGIN) {   // occlusion as margins (> 0: occluded)
+            float oc[kLightSamples] = {-1.0f, -1.0f, -1.0f};
+            for (int u = 0; u < S.n_obj_unit; ++u) {
+                const UnitF U = S.unit[u];
+                const OriginU O = origin_u(U, o32);
+                const bool do_shadow =
+                    PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));
+                fused_unit<FORCE64, COUNT, true>(S, U, O, U.grp == ogrp, do_shadow, any_trace,
+                                                 &sh, n32, &ca, sp, cnt, 15u, oc);
+            }
+#pragma unroll
+            for (int k = 0; k < kLightSamples; ++k) sh.occ[k] = oc[k] > 0.0f;
+        } else {
+            for (int u = 0; u < S.n_obj_unit; ++u) {
+                const UnitF U = S.unit[u];
+                const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
+                const bool do_shadow = PT_WAVE_ANY(!(sh.occ[0] && sh.occ[1] && sh.occ[2]));
+                fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
+                                           &ca, sp, cnt);
+            }
         }
         if (BVH && S.n_bnode) {   // the meshes: shadows as a packet, the closest ray ordered
             const bool ordered = S.bvh_depth < kBvhStack;

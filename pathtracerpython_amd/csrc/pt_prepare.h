@@ -173,8 +173,8 @@ inline void build_bvh(HostScene* H, double X) {
         BvhBuilder::Item& I = B.it[i];
         for (int a = 0; a < 3; ++a) { I.lo[a] = INFINITY; I.hi[a] = -INFINITY; }
         for (int m = 0; m < U.count; ++m) {
-            const TriD& T = H->trid[U.tri[m].t];
-            K.bvh_min_tri = std::min(K.bvh_min_tri, U.tri[m].t);
+            const TriD& T = H->trid[U.t[m]];
+            K.bvh_min_tri = std::min(K.bvh_min_tri, U.t[m]);
             K.bvh_min_obj = std::min(K.bvh_min_obj, U.obj);
             const double* vs[3] = {T.v1, T.v2, T.v3};
             for (int v = 0; v < 3; ++v)
@@ -261,6 +261,8 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     struct PlaneD { double n[3], cn, eh, eq; bool ok; };
     std::vector<PlaneD> pl(T);
     std::vector<TriB> tb(T);
+    struct TriE { float eo, ed, g; };   // barycentric bound coefficients
+    std::vector<TriE> te(T);
     const D3 Cd = d3(C[0], C[1], C[2]);
     auto l1 = [](double a, double b, double c) { return fabs(a) + fabs(b) + fabs(c); };
     const double s = 1.25;   // safety factor over the first-order bounds below
@@ -288,7 +290,8 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         PlaneD& P = pl[t];
         TriB& B = tb[t];
         B = TriB{};
-        B.t = t;
+        TriE& BE = te[t];
+        BE = TriE{};
         P.ok = (cn > 0.0) && (NN > 0.0) && isfinite(cn);
         if (!P.ok) continue;   // degenerate: the reference's NaN normal never hits
         const D3 gb = cross(e2, N) * (1.0 / NN), gc = cross(N, e1) * (1.0 / NN);
@@ -309,9 +312,9 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         // q's own error, plus 8u n1 >= 8u|q| covering the rounding of 1/q and t
         P.eq = s * 8 * u * n1 + 8 * u * n1;
         // x2: one bound for beta, gamma (error <= del/2) and alpha (<= del)
-        B.eo = f32_up(2 * (s * 8 * u * std::max(gb1 * X + fabs(cb), gc1 * X + fabs(cc)) + 8 * u));
-        B.ed = f32_up(2 * s * 8 * u * std::max(gb1, gc1));
-        B.g = f32_up(2 * std::max(gb1, gc1) * (1 + 1e-3));
+        BE.eo = f32_up(2 * (s * 8 * u * std::max(gb1 * X + fabs(cb), gc1 * X + fabs(cc)) + 8 * u));
+        BE.ed = f32_up(2 * s * 8 * u * std::max(gb1, gc1));
+        BE.g = f32_up(2 * std::max(gb1, gc1) * (1 + 1e-3));
     }
     // coplanar groups: triangle t joins the group of an earlier
     // representative r when every vertex of t lies within 1e-12 of r's plane
@@ -382,6 +385,11 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
             U.obj = d->tri_obj[t];
             U.tri[0] = tb[t];
             U.tri[1] = pair ? tb[t + 1] : TriB{};
+            U.t[0] = t;
+            U.t[1] = pair ? t + 1 : t;
+            U.eo = te[t].eo;
+            U.ed = te[t].ed;
+            U.g = te[t].g;
             if (!P.ok) {   // degenerate: dt = -inf -> certain miss, never a candidate
                 U.eh = -INFINITY;
                 U.eq = 0.f;
@@ -392,11 +400,10 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
                     eh = std::max(eh, pl[t + 1].eh) + 1e-9;
                     eq = std::max(eq, pl[t + 1].eq) + 1e-9;
                     // one bound for both members (the kernel evaluates del once per
-                    // ray and unit from tri[0]'s coefficients)
-                    const float eo = f32_up(std::max(U.tri[0].eo, U.tri[1].eo) + 2e-9);
-                    const float ed = std::max(U.tri[0].ed, U.tri[1].ed);
-                    const float g = std::max(U.tri[0].g, U.tri[1].g);
-                    for (TriB& B : U.tri) { B.eo = eo; B.ed = ed; B.g = g; }
+                    // ray and unit)
+                    U.eo = f32_up(std::max(te[t].eo, te[t + 1].eo) + 2e-9);
+                    U.ed = std::max(te[t].ed, te[t + 1].ed);
+                    U.g = std::max(te[t].g, te[t + 1].g);
                 }
                 for (int i = 0; i < 3; ++i) U.n[i] = (float)P.n[i];
                 U.cn = (float)P.cn;

@@ -75,7 +75,9 @@ int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
 // Filter self-test: random lines (origins at the eye or on triangles,
 // directions random) against every triangle; compares classify() with the
 // f64 evaluation.  out[0] = wrong certain verdicts (must be 0), out[1] =
-// ambiguous verdicts, out[2] = tests, out[3] = certain candidates.
+// ambiguous verdicts, out[2] = tests, out[3] = certain candidates, out[4] =
+// shadow tests where the margin form (margin_plane/margin_tri) differs from
+// classify_tri other than by "ambiguous" for a certain miss (must be 0).
 int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t* out) {
     HostScene H;
     if (!prepare_scene(d, &H).empty()) return -1;
@@ -83,7 +85,7 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
     std::mt19937_64 rng(seed);
     std::uniform_real_distribution<double> U(0.0, 1.0);
     std::normal_distribution<double> N(0.0, 1.0);
-    int64_t wrong = 0, amb = 0, tests = 0, cand = 0;
+    int64_t wrong = 0, amb = 0, tests = 0, cand = 0, mdiff = 0;
     const D3 C = ld3(H.k.center);
     for (int64_t i = 0; i < n_rays; ++i) {
         D3 o;
@@ -113,7 +115,7 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
                 const TriB& B = U.tri[i];
                 const float bo = i ? O.bo1 : O.bo0, co = i ? O.co1 : O.co0;
                 D3 Q; double sqd;
-                const bool h = eval64(H.trid[B.t], o, dn, &Q, &sqd);
+                const bool h = eval64(H.trid[U.t[i]], o, dn, &Q, &sqd);
                 // closest semantics
                 int st = verdict_code(classify_tri(B, pc, bo, co, d32));
                 const bool ref_c = h && sqd > kZero;
@@ -131,10 +133,17 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
                 ++tests;
                 if (st == kAmb) ++amb;
                 else if ((st == kCand) != ref_s) ++wrong;
+                // the render loop's margin form (shadow_unit_m) of the same test
+                float cm, nm, mc, ma;
+                margin_plane(U, ps, hlo, hhi, INFINITY, &cm, &nm);
+                margin_tri(B, ps, bo, co, d32, cm, nm, &mc, &ma);
+                const int ms = mc > 0.0f ? kCand : (ma >= 0.0f ? kAmb : kMiss);
+                if (ms != kAmb && (ms == kCand) != ref_s) ++wrong;
+                if (ms != st && !(st == kMiss && ms == kAmb)) ++mdiff;
             }
         }
     }
-    out[0] = wrong; out[1] = amb; out[2] = tests; out[3] = cand;
+    out[0] = wrong; out[1] = amb; out[2] = tests; out[3] = cand; out[4] = mdiff;
     return 0;
 }
 
@@ -168,7 +177,7 @@ int hc_bvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t*
                 leaf_of[q] = i;
                 const UnitF& U = H.bunit[q];
                 for (int m = 0; m < U.count; ++m) {
-                    const TriD& T = H.trid[U.tri[m].t];
+                    const TriD& T = H.trid[U.t[m]];
                     const double* vs[3] = {T.v1, T.v2, T.v3};
                     for (int v = 0; v < 3; ++v)
                         for (int a = 0; a < 3; ++a) {
@@ -198,7 +207,7 @@ int hc_bvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t*
             o = ld3(K.eye);
         } else {
             const UnitF& U = H.bunit[(size_t)(U01(rng) * K.n_bunit) % K.n_bunit];
-            const TriD& T = H.trid[U.tri[0].t];
+            const TriD& T = H.trid[U.t[0]];
             double a = U01(rng), b = U01(rng);
             if (a + b > 1) { a = 1 - a; b = 1 - b; }
             o = ld3(T.v1) * (1 - a - b) + ld3(T.v2) * a + ld3(T.v3) * b;
@@ -210,7 +219,7 @@ int hc_bvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t*
             const UnitF& U = H.bunit[q];
             for (int m = 0; m < U.count; ++m) {
                 D3 Q; double sqd;
-                if (!eval64(H.trid[U.tri[m].t], o, dn, &Q, &sqd)) continue;
+                if (!eval64(H.trid[U.t[m]], o, dn, &Q, &sqd)) continue;
                 const float R = (float)(sqrt(sqd) * (1 + 1e-6));
                 ++checked;
                 std::fill(visited.begin(), visited.end(), 0);

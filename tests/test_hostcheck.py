@@ -16,9 +16,12 @@ from pathtracerpython_amd.render import to_list_order
 
 
 def selftest(lib, packed, n, seed):
-    out = (C.c_int64 * 4)()
+    """(wrong, ambiguous, tests, candidates); also asserts that the render
+    loop's margin-form shadow verdicts agree with classify_tri."""
+    out = (C.c_int64 * 5)()
     assert lib.hc_filter_selftest(C.byref(packed.desc), C.c_int64(n), C.c_uint64(seed), out) == 0
-    return list(out)
+    assert out[4] == 0, "margin-form shadow verdicts differ from classify_tri"
+    return list(out)[:4]
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
