@@ -110,6 +110,22 @@ struct alignas(16) BNode {
     int32_t leaf;
 };
 
+// The same hierarchy for the ordered (nearest-first, per-lane stack)
+// traversals: internal nodes only, each holding both children's boxes, so a
+// step is one dependent 64-B load.  Child reference c >= 0: internal node
+// cnode[c]; c <= -2: leaf, c = ~code with code as in BNode::leaf.
+struct alignas(16) CNode {
+    float lo0[3];
+    int32_t c0;
+    float hi0[3];
+    int32_t c1;
+    float lo1[3];
+    int32_t pad0;
+    float hi1[3];
+    int32_t pad1;
+};
+constexpr int32_t kNoRef = -1;
+
 struct SceneK {
     const UnitF* unit;          // [n_unit] uniform plane units: object units (small objects, scene
                                 // order), then the light's; large meshes go to the BVH
@@ -131,7 +147,10 @@ struct SceneK {
     const BNode* bnode;         // [n_bnode] BVH of the mesh objects' units (none: n_bnode = 0)
     const UnitF* bunit;         // [n_bunit] those units in leaf order
     int32_t n_bnode, n_bunit, bvh_min_tri, bvh_min_obj;   // lowest triangle / object in it
-    int32_t bvh_depth, pad3[3];  // levels below the root (the ordered traversal's stack need)
+    int32_t bvh_depth;           // levels below the root (the ordered traversal's stack need)
+    int32_t bvh_root;            // the root as a CNode reference (0, or ~code for a leaf root)
+    int32_t pad3[2];
+    const CNode* cnode;          // [n_bnode - leaves] the two-child form of bnode
 };
 
 // ------------------------------------------------------------------ RNG --

@@ -256,16 +256,17 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         return fail(PT_ENODEV, "device is " + arch + ", this build targets gfx950 only");
     }
     HostScene& H = s->host;
-    constexpr int kArrays = 10;
+    constexpr int kArrays = 11;
     const size_t sz[kArrays] = {H.unit.size() * sizeof(UnitF), H.trid.size() * sizeof(TriD),
                                 H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
                                 H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
                                 H.light_cum.size() * sizeof(double),
                                 H.tri_grp.size() * sizeof(int32_t),
-                                H.bnode.size() * sizeof(BNode), H.bunit.size() * sizeof(UnitF)};
+                                H.bnode.size() * sizeof(BNode), H.bunit.size() * sizeof(UnitF),
+                                H.cnode.size() * sizeof(CNode)};
     const void* src[kArrays] = {H.unit.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
                                 H.mat.data(), H.light_tri.data(), H.light_cum.data(),
-                                H.tri_grp.data(), H.bnode.data(), H.bunit.data()};
+                                H.tri_grp.data(), H.bnode.data(), H.bunit.data(), H.cnode.data()};
     size_t off[kArrays], total = 0;
     for (int i = 0; i < kArrays; ++i) { off[i] = total; total += align_up(sz[i]); }
     int rc = PT_OK;
@@ -290,6 +291,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     s->dev.tri_grp = (const int32_t*)(b + off[7]);
     s->dev.bnode = (const BNode*)(b + off[8]);
     s->dev.bunit = (const UnitF*)(b + off[9]);
+    s->dev.cnode = (const CNode*)(b + off[10]);
     s->xbound = box_bound(H);
     *out = s;
     return rc;

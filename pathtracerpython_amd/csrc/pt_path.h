@@ -469,6 +469,22 @@ PT_HD D3 shadow_color(const SceneK& S, int obj, const ShadowSet& sh, Counters* c
 // node is entered when one of them meets its box within its range (shadow
 // ray k: |t| <= hhi[k]; the closest ray: |t| <= the current best's upper
 // bound), and its leaf units go through fused_unit like the uniform ones.
+// Shadow rays still open for the BVH: 0, 1 until occluded (count mode:
+// until no BVH triangle can be their lowest occluder); the last ray until no
+// BVH object can be its first occluder's.  Bit k: ray k.
+template <bool COUNT>
+PT_HD uint32_t shadow_open(const SceneK& S, const ShadowSet* sh) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        const bool open = (k == kLightSamples - 1)
+                              ? (sh->key2 > (COUNT ? S.bvh_min_tri : S.bvh_min_obj))
+                              : (COUNT ? (sh->first[k] > S.bvh_min_tri) : !sh->occ[k]);
+        m |= open ? 1u << k : 0u;
+    }
+    return m;
+}
+
 template <bool FORCE64, bool COUNT>
 PT_HD void bvh_pass(const SceneK& S, F3 o32, int ogrp, bool do_shadow, bool do_closest,
                     ShadowSet* sh, F3 n32, ClosestAcc* ca, const Spill& sp, Counters* cnt) {
@@ -494,16 +510,10 @@ PT_HD void bvh_pass(const SceneK& S, F3 o32, int ogrp, bool do_shadow, bool do_c
             const F3 h = {N.hi[0] - o32.x, N.hi[1] - o32.y, N.hi[2] - o32.z};
             uint32_t rays = 0;
             if (do_shadow) {
+                const uint32_t open = shadow_open<COUNT>(S, sh);
 #pragma unroll
-                for (int k = 0; k < kLightSamples; ++k) {
-                    // rays still open: 0, 1 until occluded (count mode: until no BVH
-                    // triangle can be their lowest occluder); the last ray until
-                    // no BVH object can be its first occluder's
-                    const bool open = (k == kLightSamples - 1)
-                                          ? (sh->key2 > (COUNT ? S.bvh_min_tri : S.bvh_min_obj))
-                                      : (COUNT ? (sh->first[k] > S.bvh_min_tri) : !sh->occ[k]);
-                    if (open && box_hit(l, h, inv[k], sh->hhi[k])) rays |= 1u << k;
-                }
+                for (int k = 0; k < kLightSamples; ++k)
+                    if (((open >> k) & 1u) && box_hit(l, h, inv[k], sh->hhi[k])) rays |= 1u << k;
             }
             if (do_closest && box_hit(l, h, invc, ca->b1)) rays |= 8u;
             if (rays && N.leaf >= 0) {
@@ -549,6 +559,11 @@ PT_HD float node_dist(const SceneK& S, int i, F3 o32, F3 inv, float R) {
     const F3 h = {N.hi[0] - o32.x, N.hi[1] - o32.y, N.hi[2] - o32.z};
     return box_dist(l, h, inv, R);
 }
+PT_HD float cbox_dist(const float* lo, const float* hi, F3 o32, F3 inv, float R) {
+    const F3 l = {lo[0] - o32.x, lo[1] - o32.y, lo[2] - o32.z};
+    const F3 h = {hi[0] - o32.x, hi[1] - o32.y, hi[2] - o32.z};
+    return box_dist(l, h, inv, R);
+}
 template <bool COUNT>
 PT_HD void bvh_closest(const SceneK& S, F3 o32, int ogrp, F3 d32, ClosestAcc* ca, const Spill& sp,
                        Counters* cnt) {
@@ -556,32 +571,103 @@ PT_HD void bvh_closest(const SceneK& S, F3 o32, int ogrp, F3 d32, ClosestAcc* ca
     int stack[kBvhStack];
     float sdist[kBvhStack];
     int top = 0;
-    int node = node_dist(S, 0, o32, inv, ca->b1) < INFINITY ? 0 : -1;
-    while (node >= 0) {
-        const BNode N = S.bnode[node];
-        int next = -1;
-        if (N.leaf >= 0) {
-            const int u0 = N.leaf >> 3, nu = N.leaf & 7;
-            for (int i = 0; i < nu; ++i) {
-                const UnitF U = S.bunit[u0 + i];
-                fused_unit<false, COUNT>(S, U, origin_u(U, o32), U.grp == ogrp, false, true,
-                                         nullptr, d32, ca, sp, cnt, 8u);
-            }
-        } else {
-            const int a = node + 1, b = S.bnode[a].skip;   // left child, right child
-            const float da = node_dist(S, a, o32, inv, ca->b1);
-            const float db = node_dist(S, b, o32, inv, ca->b1);
-            const bool near_a = da <= db;
-            const int n0 = near_a ? a : b, n1 = near_a ? b : a;
-            const float d0 = near_a ? da : db, d1 = near_a ? db : da;
-            if (d1 < INFINITY) { stack[top] = n1; sdist[top] = d1; ++top; }
-            if (d0 < INFINITY) next = n0;
-        }
-        while (next < 0 && top > 0) {   // pop, dropping nodes beyond the current bound
+    auto pop = [&]() {   // the next stacked node still within the bound, or kNoRef
+        while (top > 0) {
             --top;
-            if (sdist[top] <= ca->b1) next = stack[top];
+            if (sdist[top] <= ca->b1) return stack[top];
         }
-        node = next;
+        return kNoRef;
+    };
+    int ref = node_dist(S, 0, o32, inv, ca->b1) < INFINITY ? S.bvh_root : kNoRef;
+    while (ref != kNoRef) {
+        while (ref >= 0) {   // "while-while": descend to a leaf, then test leaves together
+            const CNode C = S.cnode[ref];
+            const float d0 = cbox_dist(C.lo0, C.hi0, o32, inv, ca->b1);
+            const float d1 = cbox_dist(C.lo1, C.hi1, o32, inv, ca->b1);
+            const bool near0 = d0 <= d1;
+            const float dn = near0 ? d0 : d1, df = near0 ? d1 : d0;
+            const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
+            if (df < INFINITY) { stack[top] = rf; sdist[top] = df; ++top; }
+            ref = dn < INFINITY ? rn : pop();
+        }
+        if (ref == kNoRef) break;
+        const int code = ~ref, u0 = code >> 3, nu = code & 7;
+        for (int i = 0; i < nu; ++i) {
+            const UnitF U = S.bunit[u0 + i];
+            fused_unit<false, COUNT>(S, U, origin_u(U, o32), U.grp == ogrp, false, true, nullptr,
+                                     d32, ca, sp, cnt, 8u);
+        }
+        ref = pop();
+    }
+}
+
+// The shadow rays of a bounce, nearest box first (the rays share their
+// origin; a box's distance is the smallest |t| of any of its rays in it):
+// an occluder near the shading point closes a ray early.  Stack entries are
+// (reference << 3 | rays that entered the box); rays closed meanwhile are
+// dropped on pop.  Ends when every ray is closed.
+template <bool COUNT>
+PT_HD void bvh_shadow(const SceneK& S, F3 o32, int ogrp, ShadowSet* sh, const Spill& sp,
+                      Counters* cnt) {
+    F3 inv[kLightSamples];
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) inv[k] = rcp_dir(sh->d32[k]);
+    int stack[kBvhStack];
+    int top = 0;
+    uint32_t rays = 0;
+    auto pop = [&]() {
+        const uint32_t open = shadow_open<COUNT>(S, sh);
+        while (top > 0) {
+            const int e = stack[--top];
+            rays = (uint32_t)e & open & 7u;
+            if (rays) return e >> 3;
+        }
+        return kNoRef;
+    };
+    {
+        const BNode R = S.bnode[0];
+        const F3 l = {R.lo[0] - o32.x, R.lo[1] - o32.y, R.lo[2] - o32.z};
+        const F3 h = {R.hi[0] - o32.x, R.hi[1] - o32.y, R.hi[2] - o32.z};
+        const uint32_t open = shadow_open<COUNT>(S, sh);
+#pragma unroll
+        for (int k = 0; k < kLightSamples; ++k)
+            if (((open >> k) & 1u) && box_hit(l, h, inv[k], sh->hhi[k])) rays |= 1u << k;
+    }
+    int ref = rays ? S.bvh_root : kNoRef;
+    while (ref != kNoRef) {
+        while (ref >= 0) {
+            const CNode C = S.cnode[ref];
+            uint32_t m0 = 0, m1 = 0;
+            float d0 = INFINITY, d1 = INFINITY;
+#pragma unroll
+            for (int k = 0; k < kLightSamples; ++k) {
+                if (!((rays >> k) & 1u)) continue;
+                const float e0 = cbox_dist(C.lo0, C.hi0, o32, inv[k], sh->hhi[k]);
+                const float e1 = cbox_dist(C.lo1, C.hi1, o32, inv[k], sh->hhi[k]);
+                m0 |= e0 < INFINITY ? 1u << k : 0u;
+                m1 |= e1 < INFINITY ? 1u << k : 0u;
+                d0 = fminf(d0, e0);
+                d1 = fminf(d1, e1);
+            }
+            const bool near0 = d0 <= d1;
+            const uint32_t mn = near0 ? m0 : m1, mf = near0 ? m1 : m0;
+            const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
+            if (mf) stack[top++] = (int)(((uint32_t)rf << 3) | mf);
+            if (mn) {
+                ref = rn;
+                rays = mn;
+            } else {
+                ref = pop();
+            }
+        }
+        if (ref == kNoRef) break;
+        const int code = ~ref, u0 = code >> 3, nu = code & 7;
+        for (int i = 0; i < nu; ++i) {
+            const UnitF U = S.bunit[u0 + i];
+            fused_unit<false, COUNT>(S, U, origin_u(U, o32), U.grp == ogrp, true, false, sh,
+                                     F3{0.f, 0.f, 0.f}, nullptr, sp, cnt, rays);
+        }
+        ref = pop();
     }
 }
 
@@ -774,10 +860,14 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
             }
         }
         if (BVH && S.n_bnode) {   // the meshes: shadows as a packet, the closest ray ordered
-            const bool ordered = S.bvh_depth < kBvhStack;
-            bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, !FORCE64 && trace && !ordered, &sh, n32,
-                                     &ca, sp, cnt);
-            if (!FORCE64 && trace && ordered) bvh_closest<COUNT>(S, o32, ogrp, n32, &ca, sp, cnt);
+            const bool ordered = !FORCE64 && S.bvh_depth < kBvhStack;
+            if (ordered) {
+                bvh_shadow<COUNT>(S, o32, ogrp, &sh, sp, cnt);
+                if (trace) bvh_closest<COUNT>(S, o32, ogrp, n32, &ca, sp, cnt);
+            } else {
+                bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, !FORCE64 && trace, &sh, n32, &ca, sp,
+                                         cnt);
+            }
         }
         if (!FORCE64 && any_trace) {
             for (int u = S.n_obj_unit; u < S.n_unit; ++u) {   // the light's units

@@ -20,6 +20,7 @@ struct HostScene {
     std::vector<UnitF> unit;
     std::vector<UnitF> bunit;
     std::vector<BNode> bnode;
+    std::vector<CNode> cnode;
     std::vector<int32_t> tri_grp;
     std::vector<TriD> trid;
     std::vector<TriS> tris;
@@ -156,6 +157,7 @@ struct BvhBuilder {
 
 inline void build_bvh(HostScene* H, double X) {
     H->bnode.clear();
+    H->cnode.clear();
     SceneK& K = H->k;
     K.n_bnode = 0;
     K.n_bunit = (int32_t)H->bunit.size();
@@ -195,6 +197,25 @@ inline void build_bvh(HostScene* H, double X) {
     H->bunit.swap(B.ordered);
     K.n_bnode = total;
     K.bvh_depth = B.depth;
+    // two-child form: internal node i has children i + 1 and bnode[i + 1].skip
+    std::vector<int32_t> cidx(total, -1);
+    for (int i = 0; i < total; ++i)
+        if (H->bnode[i].leaf < 0) cidx[i] = (int32_t)H->cnode.size(), H->cnode.push_back(CNode{});
+    auto ref = [&](int i) { return H->bnode[i].leaf >= 0 ? ~H->bnode[i].leaf : cidx[i]; };
+    for (int i = 0; i < total; ++i) {
+        if (cidx[i] < 0) continue;
+        const int a = i + 1, b = H->bnode[a].skip;
+        CNode& C = H->cnode[cidx[i]];
+        for (int k = 0; k < 3; ++k) {
+            C.lo0[k] = H->bnode[a].lo[k];
+            C.hi0[k] = H->bnode[a].hi[k];
+            C.lo1[k] = H->bnode[b].lo[k];
+            C.hi1[k] = H->bnode[b].hi[k];
+        }
+        C.c0 = ref(a);
+        C.c1 = ref(b);
+    }
+    K.bvh_root = ref(0);
 }
 
 inline D3 tri_vertex(const pt_scene_desc* d, int t, int v) {
@@ -450,6 +471,9 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     }
     for (int i = 0; i < 4; ++i) K.ortho[i] = d->ortho[i];
     K.ambient = d->ambient;
+    // leaf codes (unit offset << 3 | count) travel in stack entries as
+    // (~code << 3 | ray mask) in 32 bits
+    if (H->bunit.size() >= (size_t(1) << 24)) return "mesh too large: at most 2^24 BVH units";
     build_bvh(H, X);   // needs K.center and K.n_tri
     return "";
 }
@@ -458,6 +482,7 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
 inline void bind_host(HostScene* H) {
     H->k.unit = H->unit.data();
     H->k.bnode = H->bnode.data();
+    H->k.cnode = H->cnode.data();
     H->k.bunit = H->bunit.data();
     H->k.tri_grp = H->tri_grp.data();
     H->k.trid = H->trid.data();
