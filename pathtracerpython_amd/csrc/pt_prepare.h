@@ -32,7 +32,7 @@ struct HostScene {
 };
 
 constexpr int kBvhMinTris = 64;   // objects this large are traversed through the BVH
-constexpr int kBvhLeaf = 4;       // units per leaf (at most 7: 3 bits of BNode::leaf)
+constexpr int kBvhLeaf = 2;       // units per leaf (at most 7: 3 bits of BNode::leaf)
 constexpr int kBvhBins = 16;
 
 // outward rounding to f32
