@@ -214,12 +214,17 @@ PT_HD F3 to_f3(D3 a) { F3 r; r.x = (float)a.x; r.y = (float)a.y; r.z = (float)a.
 // in_triangle's normalisations are skipped: only the signs of c1.c2 and
 // c1.c3 matter, and a zero cross product gives 0 -> "outside", as the
 // reference's NaN does.
+// the intersection point P = o + dn t of utils.py:118-120 (no range test)
+PT_HD D3 plane_point(const TriD& T, D3 o, D3 dn) {
+    const D3 vp = ld3(T.vp);
+    const double t = (T.cvp - dot(vp, o)) * rcp_d(dot(vp, dn));
+    return o + dn * t;
+}
 PT_HD bool eval64(const TriD& T, D3 o, D3 dn, D3* P, double* sqd) {
     const D3 vp = ld3(T.vp);
     const double den = dot(dn, vp);
     if (!(fabs(den) > kZero)) return false;
-    const double t = (T.cvp - dot(vp, o)) * rcp_d(dot(vp, dn));
-    const D3 p = o + dn * t;
+    const D3 p = plane_point(T, o, dn);
     const D3 c1 = cross(ld3(T.e12), p - ld3(T.v2));
     const D3 c2 = cross(ld3(T.e23), p - ld3(T.v3));
     const D3 c3 = cross(ld3(T.e31), p - ld3(T.v1));

@@ -42,7 +42,12 @@ PT_HD void bump(Counters* c, uint32_t Counters::*f, uint32_t v) {
 // compiler from using scalar loads for the uniform triangle reads.)  Slots:
 //   0..8  light sample points L_k       9..11  next-ray direction (as the
 //   12..14 ray origin P                        reference holds it, unnormalised)
-//   15..17 primary direction d0
+//   15..16 primary direction d0 (x, y; its z is -eye.z)
+//   17..19 primary hit point P0
+// The path's origin P and the cached primary hit P0 live here rather than in
+// VGPRs across the bounce loop: 20 slots x 256 lanes = 40 KB per block, the
+// 160 KB of a CU at 4 blocks (the register allocator otherwise spills them to
+// scratch, which costs ~1.2 GB of HBM writes per K2 launch).
 struct Spill {
     double* base;
     int stride;
@@ -51,8 +56,8 @@ struct Spill {
     PT_HD D3 get3(int i) const { return d3(get(i), get(i + 1), get(i + 2)); }
     PT_HD void put3(int i, D3 v) const { put(i, v.x); put(i + 1, v.y); put(i + 2, v.z); }
 };
-constexpr int kSpillSlots = 18;
-constexpr int kSpL = 0, kSpNd = 9, kSpP = 12, kSpD0 = 15;
+constexpr int kSpillSlots = 20;
+constexpr int kSpL = 0, kSpNd = 9, kSpP = 12, kSpD0 = 15, kSpP0 = 17;
 
 // ----------------------------------------------------------- closest hit --
 // intersect_objects (main.py:83-122): the triangle whose intersection has the
@@ -169,9 +174,12 @@ PT_HD void bvh_rescan(const SceneK& S, D3 o, D3 dn, float R, int* best, double* 
 // certainly the closest when its interval ends before every other one
 // starts; otherwise rescan exactly in f64.  Returns the triangle (-1 = None)
 // and the hit point exactly as the reference computes it.
+// P_home: when given, the hit point also goes to that spill slot (the
+// render loop's next origin), written where it is computed so that it is not
+// carried in VGPRs across the join.
 template <bool FORCE64, bool COUNT, bool BVH = true>
 PT_HD int closest_finish(const SceneK& S, const ClosestAcc& c, D3 o, D3 dn, D3* P,
-                         Counters* cnt) {
+                         Counters* cnt, const Spill* P_home = nullptr) {
     int best = c.i1;
     const bool decided = !FORCE64 && ((c.i1 < 0) || (c.b1 < c.a2));
     if (!decided) {
@@ -202,7 +210,10 @@ PT_HD int closest_finish(const SceneK& S, const ClosestAcc& c, D3 o, D3 dn, D3* 
             bvh_rescan(S, o, dn, c.b1, &best, &bsq);
         }
     }
-    if (best >= 0) {
+    if (P_home) {   // branch-free (the winner passed eval64): a miss writes a point nobody reads
+        *P = plane_point(S.trid[best >= 0 ? best : 0], o, dn);
+        P_home->put3(kSpP, *P);
+    } else if (best >= 0) {
         double sqd;
         eval64(S.trid[best], o, dn, P, &sqd);
     }
@@ -792,16 +803,19 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
     int si = 0;
     int b = 0;
     int tri = tri0;
-    D3 P = P0;
     double k = 1.0;
     bool active = true;
-    sp.put3(kSpD0, d0);
+    sp.put(kSpD0, d0.x);
+    sp.put(kSpD0 + 1, d0.y);
+    sp.put3(kSpP0, P0);
+    sp.put3(kSpP, P0);
     sp.put3(kSpNd, d0);   // incoming direction of bounce 0 (main.py:191)
     if (COUNT) {   // the cached primary trace, counted per sample
         bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
         bump<COUNT>(cnt, &Counters::ray_bounces, 1);
     }
     while (active) {
+        const D3 P = sp.get3(kSpP);   // this bounce's origin
         const uint32_t sample = (uint32_t)(J.sample0 + si * J.sample_stride);
         const int obj = S.tri_obj[tri];
         const TriS R = S.tris[tri];
@@ -832,7 +846,6 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
             else kk = kn / q;
         }
         // one pass: 3 shadow rays + the next ray's closest hit, same origin
-        sp.put3(kSpP, P);
         sp.put3(kSpNd, nd);
         const F3 o32 = to_f3(P - ld3(S.center));
         const F3 n32 = to_f3(unit(nd));
@@ -882,8 +895,10 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         bool done = !trace;
         if (trace) {
             D3 Pn;
+            // the hit point goes straight to the origin slot (overwritten below
+            // when the path ends here)
             const int tn = closest_finish<FORCE64, COUNT, BVH>(S, ca, sp.get3(kSpP),
-                                                          unit(sp.get3(kSpNd)), &Pn, cnt);
+                                                          unit(sp.get3(kSpNd)), &Pn, cnt, &sp);
             if (tn < 0) {
                 bump<COUNT>(cnt, &Counters::escapes, 1);
                 done = true;
@@ -892,7 +907,6 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
                 bump<COUNT>(cnt, &Counters::light_hits, 1);
                 done = true;
             } else {
-                P = Pn;
                 tri = tn;
                 ++b;
             }
@@ -904,9 +918,9 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
             } else {   // next sample from the cached primary hit
                 b = 0;
                 tri = tri0;
-                P = P0;
                 k = 1.0;
-                sp.put3(kSpNd, sp.get3(kSpD0));
+                sp.put3(kSpP, sp.get3(kSpP0));
+                sp.put3(kSpNd, d3(sp.get(kSpD0), sp.get(kSpD0 + 1), 0.0 - S.eye[2]));
                 if (COUNT) {
                     bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
                     bump<COUNT>(cnt, &Counters::ray_bounces, 1);
