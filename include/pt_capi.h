@@ -45,6 +45,9 @@ extern "C" {
 #define PT_FLAG_COUNT (1u << 2)        /* fill pt_stats counters (slower) */
 #define PT_FLAG_OUT_F64 (1u << 3)      /* framebuffer elements are float64
                                           (default float32)              */
+#define PT_FLAG_MEGAKERNEL (1u << 4)   /* scenes with a BVH: render with the
+                                          single kernel instead of the
+                                          wavefront kernels (same result) */
 
 /*
  * Flattened scene, as produced by scene_reader.Scene

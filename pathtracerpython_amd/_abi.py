@@ -13,6 +13,7 @@ PT_FLAG_RR = 1 << 0
 PT_FLAG_FORCE_F64 = 1 << 1
 PT_FLAG_COUNT = 1 << 2
 PT_FLAG_OUT_F64 = 1 << 3
+PT_FLAG_MEGAKERNEL = 1 << 4
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)

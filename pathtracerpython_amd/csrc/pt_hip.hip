@@ -16,6 +16,7 @@
 #include <string>
 
 #include "pt_path.h"
+#include "pt_wavefront.h"
 #include "pt_prepare.h"
 #include "pt_image.h"
 #include "pt_ingest.h"
@@ -63,6 +64,66 @@ __device__ __forceinline__ void flush_counters(const Counters& c, StatsDev* st) 
     }
 }
 
+// Work-item -> (pixel, sample slice) of a launch: `split` adjacent work-items
+// share a pixel and stride its samples; the primary ray of main.py:191
+// (make_screen_pts / make_rays, utils.py:55-69).
+struct SlotJob {
+    LaneJob J;
+    D3 d0;
+    int32_t row_local, ix;
+    uint32_t c;
+    bool valid;
+};
+__device__ __forceinline__ SlotJob slot_job(const SceneK& S, const RenderK& R, uint32_t tid) {
+    SlotJob j;
+    const uint32_t pl = tid >> R.split_log2;
+    j.c = tid & (R.split - 1u);
+    j.valid = pl < R.npix;
+    j.row_local = 0;
+    j.ix = 0;
+    j.d0 = d3(0, 0, 0);
+    j.J = LaneJob{};
+    if (j.valid) {
+        j.row_local = (int32_t)(pl / (uint32_t)R.W);
+        j.ix = (int32_t)pl - j.row_local * R.W;
+        const int32_t iy = R.first_row + j.row_local * R.row_step;
+        const D3 eye = ld3(S.eye);
+        const double x = linspace_at(S.ortho[0], S.ortho[2], R.W, j.ix);
+        const double y = linspace_at(S.ortho[1], S.ortho[3], R.H, iy);
+        j.d0 = d3(x - eye.x, y - eye.y, 0.0 - eye.z);
+        const int32_t c = (int32_t)j.c, sp = (int32_t)R.split;
+        j.J.seed = R.seed;
+        j.J.pixel = (uint32_t)j.ix * (uint32_t)R.H + (uint32_t)iy;
+        j.J.sample0 = R.sample_begin + c;
+        j.J.sample_stride = sp;
+        j.J.n_samples = (c < R.spp) ? (R.spp - c + sp - 1) / sp : 0;
+        j.J.bounces = R.bounces;
+        j.J.rr_depth = R.rr_depth;
+    }
+    return j;
+}
+
+// Sum of a pixel's sample colours over its `split` work-items (fixed xor
+// order: deterministic), / spp (main.py:277), into the framebuffer.
+__device__ __forceinline__ void store_pixel(const RenderK& R, const SlotJob& j, D3 acc, void* out) {
+    for (uint32_t m = 1; m < R.split; m <<= 1) {
+        acc.x += __shfl_xor(acc.x, (int)m);
+        acc.y += __shfl_xor(acc.y, (int)m);
+        acc.z += __shfl_xor(acc.z, (int)m);
+    }
+    if (j.valid && j.c == 0) {   // pixel_color_list[i] / how_many_rays, main.py:277
+        const double inv = (double)R.spp;
+        const size_t e = ((size_t)(R.n_rows - 1 - j.row_local) * (size_t)R.W + (size_t)j.ix) * 3;
+        if (R.out_f64) {
+            double* o = (double*)out + e;
+            o[0] = acc.x / inv; o[1] = acc.y / inv; o[2] = acc.z / inv;
+        } else {
+            float* o = (float*)out + e;
+            o[0] = (float)(acc.x / inv); o[1] = (float)(acc.y / inv); o[2] = (float)(acc.z / inv);
+        }
+    }
+}
+
 template <bool FORCE64, bool COUNT, bool BVH>
 // 4 waves/SIMD (<= 128 VGPRs, a little scratch spill outside the triangle
 // loops): 9.5 ms vs 10.8 ms at 3 waves and 15.3 ms at 2 on the 512^2 x 64spp
@@ -71,6 +132,8 @@ __global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __
                                                 StatsDev* __restrict__ st) {
     __shared__ double spill[kSpillSlots][256];
     const Spill sp{&spill[0][threadIdx.x], 256};
+    // (slot_job's mapping written out: the register allocation of this kernel
+    // is sensitive to what stays live across the render loop)
     const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t pl = tid >> R.split_log2;
     const uint32_t c = tid & (R.split - 1u);
@@ -82,7 +145,6 @@ __global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __
         row_local = (int32_t)(pl / (uint32_t)R.W);
         ix = (int32_t)pl - row_local * R.W;
         const int32_t iy = R.first_row + row_local * R.row_step;
-        // make_screen_pts / make_rays, utils.py:55-69
         const D3 eye = ld3(S.eye);
         const double x = linspace_at(S.ortho[0], S.ortho[2], R.W, ix);
         const double y = linspace_at(S.ortho[1], S.ortho[3], R.H, iy);
@@ -101,23 +163,153 @@ __global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __
         if (ns > 0 && R.bounces > 0) tri0 = closest<FORCE64, false, BVH>(S, eye, d0, -1, sp, &P0, &cnt);
         acc = render_lane<FORCE64, COUNT, BVH>(S, J, d0, tri0, P0, sp, &cnt);
     }
-    for (uint32_t m = 1; m < R.split; m <<= 1) {
-        acc.x += __shfl_xor(acc.x, (int)m);
-        acc.y += __shfl_xor(acc.y, (int)m);
-        acc.z += __shfl_xor(acc.z, (int)m);
-    }
-    if (valid && c == 0) {   // pixel_color_list[i] / how_many_rays, main.py:277
-        const double inv = (double)R.spp;
-        const size_t e = ((size_t)(R.n_rows - 1 - row_local) * (size_t)R.W + (size_t)ix) * 3;
-        if (R.out_f64) {
-            double* o = (double*)out + e;
-            o[0] = acc.x / inv; o[1] = acc.y / inv; o[2] = acc.z / inv;
+    SlotJob j;
+    j.valid = valid;
+    j.c = c;
+    j.row_local = row_local;
+    j.ix = ix;
+    store_pixel(R, j, acc, out);
+    flush_counters<COUNT>(cnt, st);
+}
+
+// ------------------------------------------------- wavefront (BVH scenes) --
+// pt_wavefront.h.  Queue counters: [0] shadow count, [1] shadow head,
+// [2] closest count, [3] closest head; lists[0..slots) shadow, then closest.
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {   // set bits of m below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// wave-aggregated append: one atomic per wave
+__device__ __forceinline__ void wf_append(bool want, int32_t* counter, int32_t* list, int32_t v) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return;
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    int32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(counter, (int32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    if (want) list[base + (int32_t)lanes_below(m)] = v;
+}
+// wave-aggregated fetch of the next list positions for the lanes that need one
+__device__ __forceinline__ int32_t wf_fetch(bool need, int32_t* head) {
+    const uint64_t m = __ballot(need);
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    int32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(head, (int32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    return base + (int32_t)lanes_below(m);
+}
+
+__global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t step,
+                                                  WfPath* __restrict__ W, WfShadowQ* __restrict__ SQ,
+                                                  WfClosestQ* __restrict__ CQ,
+                                                  int32_t* __restrict__ lists, int32_t* counters,
+                                                  uint32_t slots) {
+    const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
+    const SlotJob j = slot_job(S, R, tid);
+    uint32_t want = 0;
+    if (step == 0) {
+        if (j.valid) {
+            want = wf_start(S, j.J, j.d0, &W[tid], &CQ[tid]);
         } else {
-            float* o = (float*)out + e;
-            o[0] = (float)(acc.x / inv); o[1] = (float)(acc.y / inv); o[2] = (float)(acc.z / inv);
+            W[tid].acc[0] = W[tid].acc[1] = W[tid].acc[2] = 0.0;
+            W[tid].state = kWfDone;
+        }
+    } else if (j.valid && W[tid].state != kWfDone) {
+        want = wf_shade(S, j.J, j.d0, &W[tid], &SQ[tid], &CQ[tid]);
+    }
+    wf_append((want & kWfWantShadow) != 0, &counters[0], lists, (int32_t)tid);
+    wf_append((want & kWfWantClosest) != 0, &counters[2], lists + slots, (int32_t)tid);
+}
+
+// Persistent walk kernels: a work-item holds one query at a time and takes
+// the next one from the list as soon as its walk ends.
+__global__ __launch_bounds__(256) void k_wf_shadow(SceneK S, WfPath* __restrict__ W,
+                                                   WfShadowQ* __restrict__ SQ,
+                                                   const int32_t* __restrict__ list, int32_t* counters) {
+    const int32_t count = counters[0];
+    int32_t slot = -1;
+    bool exhausted = false;
+    ShadowSet sh;
+    ShadowTrav T;
+    ShadowStack K;
+    while (true) {
+        const bool need = slot < 0 && !exhausted;
+        if (__any(need)) {
+            const int32_t i = wf_fetch(need, &counters[1]);
+            if (need) {
+                if (i < count) {
+                    slot = list[i];
+                    F3 o32;
+                    int ogrp;
+                    wf_get_shadow(S, SQ[slot], &o32, &ogrp, &sh);
+                    strav_init<false>(T, S, o32, ogrp, &sh);
+                } else {
+                    exhausted = true;
+                }
+            }
+        }
+        if (__all(slot < 0)) break;
+        if (slot >= 0) {
+            const Spill sp{W[slot].sp, 1};
+            if (strav_step<false>(T, K, S, &sh, sp, nullptr)) {
+                int occ = 0;
+#pragma unroll
+                for (int k = 0; k < kLightSamples; ++k) occ |= sh.occ[k] ? 1 << k : 0;
+                SQ[slot].occ = occ;
+                SQ[slot].leak = sh.leak;
+                slot = -1;
+            }
         }
     }
-    flush_counters<COUNT>(cnt, st);
+}
+
+__global__ __launch_bounds__(256) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
+                                                    WfClosestQ* __restrict__ CQ,
+                                                    const int32_t* __restrict__ list, int32_t* counters) {
+    const int32_t count = counters[2];
+    int32_t slot = -1;
+    bool exhausted = false;
+    ClosestAcc ca = closest_init();
+    ClosestTrav T;
+    ClosestStack K;
+    while (true) {
+        const bool need = slot < 0 && !exhausted;
+        if (__any(need)) {
+            const int32_t i = wf_fetch(need, &counters[3]);
+            if (need) {
+                if (i < count) {
+                    slot = list[i];
+                    const WfClosestQ q = CQ[slot];
+                    ca = wf_get_acc(q);
+                    ctrav_init(T, S, F3{q.o[0], q.o[1], q.o[2]}, q.ogrp, F3{q.d[0], q.d[1], q.d[2]},
+                               ca.b1);
+                } else {
+                    exhausted = true;
+                }
+            }
+        }
+        if (__all(slot < 0)) break;
+        if (slot >= 0) {
+            const Spill sp{W[slot].sp, 1};
+            if (ctrav_step<false>(T, K, S, &ca, sp, nullptr)) {
+                CQ[slot].a1 = ca.a1;
+                CQ[slot].a2 = ca.a2;
+                CQ[slot].b1 = ca.b1;
+                CQ[slot].i1 = ca.i1;
+                slot = -1;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_wf_final(SceneK S, RenderK R, const WfPath* __restrict__ W,
+                                                  void* __restrict__ out) {
+    const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
+    const SlotJob j = slot_job(S, R, tid);
+    const D3 acc = j.valid ? ld3(W[tid].acc) : d3(0, 0, 0);
+    store_pixel(R, j, acc, out);
 }
 
 __global__ __launch_bounds__(256) void k_intersect(SceneK S, const double* __restrict__ rays,
@@ -170,6 +362,10 @@ struct pt_scene {
     hipStream_t stream = nullptr;  // pt_render's own stream
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    // wavefront path (BVH scenes): path records, query records, query lists
+    // and counters, one allocation grown on demand
+    void* wf = nullptr;
+    size_t wf_slots = 0;
 };
 
 namespace {
@@ -231,6 +427,7 @@ void pt_scene_destroy(pt_scene* s) {
         if (s->blob) (void)hipFree(s->blob);
         if (s->stats) (void)hipFree(s->stats);
         if (s->out_dev) (void)hipFree(s->out_dev);
+        if (s->wf) (void)hipFree(s->wf);
         if (s->ev0) (void)hipEventDestroy(s->ev0);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
         if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -334,6 +531,54 @@ static uint32_t choose_split(uint32_t npix, int32_t spp) {
     return s;
 }
 
+// The wavefront render of a BVH scene (pt_wavefront.h): per step one shade
+// launch over the path slots, then the two persistent walk launches over the
+// queries it appended.  A slot runs at most n_samples x bounces bounces plus
+// the primary ray, so that many steps (+1 to finish the last bounce) drain
+// every slot; steps after that would find no work.
+static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_dev, hipStream_t st) {
+    const size_t slots = (size_t)grid.x * 256;
+    const size_t sz_w = slots * sizeof(WfPath), sz_s = slots * sizeof(WfShadowQ),
+                 sz_c = slots * sizeof(WfClosestQ), sz_l = 2 * slots * sizeof(int32_t);
+    const size_t off_s = sz_w, off_c = off_s + sz_s, off_l = off_c + sz_c, off_n = off_l + sz_l;
+    const size_t need = off_n + 256;
+    if (slots > s->wf_slots) {
+        if (s->wf) (void)hipFree(s->wf);
+        s->wf = nullptr;
+        s->wf_slots = 0;
+        if (hipMalloc(&s->wf, need) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc wavefront buffers");
+        s->wf_slots = slots;
+    }
+    char* b = (char*)s->wf;
+    WfPath* W = (WfPath*)b;
+    WfShadowQ* SQ = (WfShadowQ*)(b + off_s);
+    WfClosestQ* CQ = (WfClosestQ*)(b + off_c);
+    int32_t* lists = (int32_t*)(b + off_l);
+    int32_t* counters = (int32_t*)(b + off_n);
+    // persistent walk grids: enough work-items to fill the chip, no more
+    // than the queries could use
+    const unsigned walk_blocks = std::min<unsigned>(grid.x, 4096u);
+    const int32_t per_slot = (R.spp + (int32_t)R.split - 1) / (int32_t)R.split;
+    const int32_t steps = per_slot * R.bounces + 2;
+    HIPCHK(hipEventRecord(s->ev0, st));
+    for (int32_t step = 0; step < steps; ++step) {
+        HIPCHK(hipMemsetAsync(counters, 0, 4 * sizeof(int32_t), st));
+        hipLaunchKernelGGL(k_wf_shade, grid, dim3(256), 0, st, s->dev, R, step, W, SQ, CQ, lists,
+                           counters, (uint32_t)slots);
+        if (step + 1 < steps) {
+            hipLaunchKernelGGL(k_wf_shadow, dim3(walk_blocks), dim3(256), 0, st, s->dev, W, SQ,
+                               (const int32_t*)lists, counters);
+            hipLaunchKernelGGL(k_wf_closest, dim3(walk_blocks), dim3(256), 0, st, s->dev, W, CQ,
+                               (const int32_t*)(lists + slots), counters);
+        }
+    }
+    hipLaunchKernelGGL(k_wf_final, grid, dim3(256), 0, st, s->dev, R, (const WfPath*)W, out_dev);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(s->ev1, st));
+    s->timed = true;
+    return PT_OK;
+}
+
 int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void* stream,
                      pt_stats* stats) {
     if (!s) return fail(PT_EINVAL, "null scene");
@@ -360,6 +605,16 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
     const bool count = (p->flags & PT_FLAG_COUNT) != 0;
     const bool f64 = (p->flags & PT_FLAG_FORCE_F64) != 0;
+    // BVH scenes render through the wavefront kernels unless the caller asks
+    // for the single kernel (and for counting / forced-f64 launches, which
+    // only the single kernel implements)
+    const bool wavefront = s->dev.n_bnode > 0 && !count && !f64 &&
+                           !(p->flags & PT_FLAG_MEGAKERNEL) && s->dev.bvh_depth < kBvhStack;
+    if (wavefront) {
+        rc = render_wavefront(s, R, grid, out_dev, st);
+        if (!rc && stats) memset(stats, 0, sizeof(*stats));
+        return rc;
+    }
     if (count) HIPCHK(hipMemsetAsync(s->stats, 0, sizeof(StatsDev), st));
     HIPCHK(hipEventRecord(s->ev0, st));
     if (f64) {

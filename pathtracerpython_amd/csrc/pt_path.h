@@ -575,40 +575,123 @@ PT_HD float cbox_dist(const float* lo, const float* hi, F3 o32, F3 inv, float R)
     const F3 h = {hi[0] - o32.x, hi[1] - o32.y, hi[2] - o32.z};
     return box_dist(l, h, inv, R);
 }
+// The ordered traversals are resumable: a traversal object holds the walk's
+// state and step() runs one "while-while" round (walk internal nodes to the
+// next leaf its lines reach, test that leaf, pop the next entry).  The
+// single-kernel path runs a traversal to completion in place; the wavefront
+// query kernels (pt_wavefront.h) keep one per lane and refill a lane with the
+// next query as soon as its traversal ends.
+//
+// Per-lane stack (scratch) with its top entry cached in registers: a pop
+// takes the cached entry and starts the refill load, whose result is only
+// needed at the next pop.
+struct ClosestTrav {
+    F3 o32, d32, inv;
+    int ogrp;
+    int ref;                  // next node / leaf (kNoRef: done)
+    int lu, le;               // ctrav_step1: units [lu, le) of the open leaf
+    int top;                  // entries in the scratch part
+    int tref;                 // cached top (kNoRef: empty)
+    float tdist;
+};
+// The stack arrays live outside the traversal object (a local array indexed
+// at run time is scratch memory; inside the object it would drag the whole
+// object — origin, inverse direction — to scratch with it).
+struct ClosestStack {
+    int ref[kBvhStack];
+    float dist[kBvhStack];
+};
+PT_HD void ctrav_push(ClosestTrav& T, ClosestStack& K, int r, float d) {
+    if (T.tref != kNoRef) { K.ref[T.top] = T.tref; K.dist[T.top] = T.tdist; ++T.top; }
+    T.tref = r;
+    T.tdist = d;
+}
+PT_HD int ctrav_pop(ClosestTrav& T, ClosestStack& K, float bound) {   // next node within the bound, or kNoRef
+    while (T.tref != kNoRef) {
+        const int r = T.tref;
+        const float d = T.tdist;
+        if (T.top > 0) { --T.top; T.tref = K.ref[T.top]; T.tdist = K.dist[T.top]; }
+        else T.tref = kNoRef;
+        if (d <= bound) return r;
+    }
+    return kNoRef;
+}
+PT_HD void ctrav_init(ClosestTrav& T, const SceneK& S, F3 o32, int ogrp, F3 d32, float bound) {
+    T.o32 = o32;
+    T.d32 = d32;
+    T.inv = rcp_dir(d32);
+    T.ogrp = ogrp;
+    T.top = 0;
+    T.tref = kNoRef;
+    T.tdist = INFINITY;
+    T.ref = node_dist(S, 0, o32, T.inv, bound) < INFINITY ? S.bvh_root : kNoRef;
+    T.lu = T.le = 0;
+}
+// one round; returns true when the traversal has ended
 template <bool COUNT>
-PT_HD void bvh_closest(const SceneK& S, F3 o32, int ogrp, F3 d32, ClosestAcc* ca, const Spill& sp,
-                       Counters* cnt) {
-    const F3 inv = rcp_dir(d32);
-    int stack[kBvhStack];
-    float sdist[kBvhStack];
-    int top = 0;
-    auto pop = [&]() {   // the next stacked node still within the bound, or kNoRef
-        while (top > 0) {
-            --top;
-            if (sdist[top] <= ca->b1) return stack[top];
-        }
-        return kNoRef;
-    };
-    int ref = node_dist(S, 0, o32, inv, ca->b1) < INFINITY ? S.bvh_root : kNoRef;
-    while (ref != kNoRef) {
-        while (ref >= 0) {   // "while-while": descend to a leaf, then test leaves together
-            const CNode C = S.cnode[ref];
-            const float d0 = cbox_dist(C.lo0, C.hi0, o32, inv, ca->b1);
-            const float d1 = cbox_dist(C.lo1, C.hi1, o32, inv, ca->b1);
-            const bool near0 = d0 <= d1;
-            const float dn = near0 ? d0 : d1, df = near0 ? d1 : d0;
-            const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
-            if (df < INFINITY) { stack[top] = rf; sdist[top] = df; ++top; }
-            ref = dn < INFINITY ? rn : pop();
-        }
-        if (ref == kNoRef) break;
+PT_HD bool ctrav_step(ClosestTrav& T, ClosestStack& K, const SceneK& S, ClosestAcc* ca,
+                      const Spill& sp, Counters* cnt) {
+    int ref = T.ref;
+    while (ref >= 0) {   // "while-while": descend to a leaf, then test leaves together
+        const CNode C = S.cnode[ref];
+        const float d0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv, ca->b1);
+        const float d1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv, ca->b1);
+        const bool near0 = d0 <= d1;
+        const float dn = near0 ? d0 : d1, df = near0 ? d1 : d0;
+        const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
+        if (df < INFINITY) ctrav_push(T, K, rf, df);
+        ref = dn < INFINITY ? rn : ctrav_pop(T, K, ca->b1);
+    }
+    if (ref != kNoRef) {
         const int code = ~ref, u0 = code >> 3, nu = code & 7;
         for (int i = 0; i < nu; ++i) {
             const UnitF U = S.bunit[u0 + i];
-            fused_unit<false, COUNT>(S, U, origin_u(U, o32), U.grp == ogrp, false, true, nullptr,
-                                     d32, ca, sp, cnt, 8u);
+            fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, false, true, nullptr,
+                                     T.d32, ca, sp, cnt, 8u);
         }
-        ref = pop();
+        ref = ctrav_pop(T, K, ca->b1);
+    }
+    T.ref = ref;
+    return ref == kNoRef;
+}
+// The same walk in quanta of one node or one leaf unit ("if-if"): the
+// wavefront walk kernels call it once per loop turn, so every turn costs the
+// same and a lane whose walk ends is refilled at the next turn.  Leaf refs
+// are <= -2 (leaf codes have a unit count >= 1).
+template <bool COUNT>
+PT_HD bool ctrav_step1(ClosestTrav& T, ClosestStack& K, const SceneK& S, ClosestAcc* ca,
+                       const Spill& sp, Counters* cnt) {
+    if (T.lu < T.le) {   // one unit of the open leaf
+        const UnitF U = S.bunit[T.lu];
+        ++T.lu;
+        fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, false, true, nullptr,
+                                 T.d32, ca, sp, cnt, 8u);
+        if (T.lu == T.le) T.ref = ctrav_pop(T, K, ca->b1);
+    } else if (T.ref >= 0) {   // one internal node
+        const CNode C = S.cnode[T.ref];
+        const float d0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv, ca->b1);
+        const float d1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv, ca->b1);
+        const bool near0 = d0 <= d1;
+        const float dn = near0 ? d0 : d1, df = near0 ? d1 : d0;
+        const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
+        if (df < INFINITY) ctrav_push(T, K, rf, df);
+        T.ref = dn < INFINITY ? rn : ctrav_pop(T, K, ca->b1);
+    }
+    if (T.lu >= T.le && T.ref <= -2) {   // arrived at a leaf: open it
+        const int code = ~T.ref;
+        T.lu = code >> 3;
+        T.le = T.lu + (code & 7);
+        T.ref = kNoRef;
+    }
+    return T.lu >= T.le && T.ref == kNoRef;
+}
+template <bool COUNT>
+PT_HD void bvh_closest(const SceneK& S, F3 o32, int ogrp, F3 d32, ClosestAcc* ca, const Spill& sp,
+                       Counters* cnt) {
+    ClosestTrav T;
+    ClosestStack K;
+    ctrav_init(T, S, o32, ogrp, d32, ca->b1);
+    while (!ctrav_step<COUNT>(T, K, S, ca, sp, cnt)) {
     }
 }
 
@@ -617,68 +700,151 @@ PT_HD void bvh_closest(const SceneK& S, F3 o32, int ogrp, F3 d32, ClosestAcc* ca
 // an occluder near the shading point closes a ray early.  Stack entries are
 // (reference << 3 | rays that entered the box); rays closed meanwhile are
 // dropped on pop.  Ends when every ray is closed.
-template <bool COUNT>
-PT_HD void bvh_shadow(const SceneK& S, F3 o32, int ogrp, ShadowSet* sh, const Spill& sp,
-                      Counters* cnt) {
+struct ShadowTrav {
+    F3 o32;
     F3 inv[kLightSamples];
-#pragma unroll
-    for (int k = 0; k < kLightSamples; ++k) inv[k] = rcp_dir(sh->d32[k]);
-    int stack[kBvhStack];
-    int top = 0;
-    uint32_t rays = 0;
-    auto pop = [&]() {
-        const uint32_t open = shadow_open<COUNT>(S, sh);
-        while (top > 0) {
-            const int e = stack[--top];
-            rays = (uint32_t)e & open & 7u;
-            if (rays) return e >> 3;
-        }
-        return kNoRef;
-    };
-    {
-        const BNode R = S.bnode[0];
-        const F3 l = {R.lo[0] - o32.x, R.lo[1] - o32.y, R.lo[2] - o32.z};
-        const F3 h = {R.hi[0] - o32.x, R.hi[1] - o32.y, R.hi[2] - o32.z};
-        const uint32_t open = shadow_open<COUNT>(S, sh);
-#pragma unroll
-        for (int k = 0; k < kLightSamples; ++k)
-            if (((open >> k) & 1u) && box_hit(l, h, inv[k], sh->hhi[k])) rays |= 1u << k;
+    int ogrp;
+    int ref;                  // next node / leaf (kNoRef: done)
+    uint32_t rays;            // the lines that entered ref's box
+    int lu, le;               // strav_step1: units [lu, le) of the open leaf
+    int top;
+    int tc;                   // cached top entry (0: empty; a real entry has a ray bit)
+};
+struct ShadowStack {
+    int e[kBvhStack];
+};
+template <bool COUNT>
+PT_HD int strav_pop(ShadowTrav& T, ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
+    const uint32_t open = shadow_open<COUNT>(S, sh);
+    while (T.tc != 0) {
+        const int e = T.tc;
+        T.tc = T.top > 0 ? K.e[--T.top] : 0;
+        T.rays = (uint32_t)e & open & 7u;
+        if (T.rays) return e >> 3;
     }
-    int ref = rays ? S.bvh_root : kNoRef;
-    while (ref != kNoRef) {
-        while (ref >= 0) {
-            const CNode C = S.cnode[ref];
-            uint32_t m0 = 0, m1 = 0;
-            float d0 = INFINITY, d1 = INFINITY;
+    return kNoRef;
+}
+template <bool COUNT>
+PT_HD void strav_init(ShadowTrav& T, const SceneK& S, F3 o32, int ogrp, const ShadowSet* sh) {
+    T.o32 = o32;
+    T.ogrp = ogrp;
 #pragma unroll
-            for (int k = 0; k < kLightSamples; ++k) {
-                if (!((rays >> k) & 1u)) continue;
-                const float e0 = cbox_dist(C.lo0, C.hi0, o32, inv[k], sh->hhi[k]);
-                const float e1 = cbox_dist(C.lo1, C.hi1, o32, inv[k], sh->hhi[k]);
-                m0 |= e0 < INFINITY ? 1u << k : 0u;
-                m1 |= e1 < INFINITY ? 1u << k : 0u;
-                d0 = fminf(d0, e0);
-                d1 = fminf(d1, e1);
-            }
-            const bool near0 = d0 <= d1;
-            const uint32_t mn = near0 ? m0 : m1, mf = near0 ? m1 : m0;
-            const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
-            if (mf) stack[top++] = (int)(((uint32_t)rf << 3) | mf);
-            if (mn) {
-                ref = rn;
-                rays = mn;
-            } else {
-                ref = pop();
-            }
+    for (int k = 0; k < kLightSamples; ++k) T.inv[k] = rcp_dir(sh->d32[k]);
+    T.top = 0;
+    T.tc = 0;
+    uint32_t rays = 0;
+    const BNode R = S.bnode[0];
+    const F3 l = {R.lo[0] - o32.x, R.lo[1] - o32.y, R.lo[2] - o32.z};
+    const F3 h = {R.hi[0] - o32.x, R.hi[1] - o32.y, R.hi[2] - o32.z};
+    const uint32_t open = shadow_open<COUNT>(S, sh);
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k)
+        if (((open >> k) & 1u) && box_hit(l, h, T.inv[k], sh->hhi[k])) rays |= 1u << k;
+    T.rays = rays;
+    T.ref = rays ? S.bvh_root : kNoRef;
+    T.lu = T.le = 0;
+}
+template <bool COUNT>
+PT_HD bool strav_step(ShadowTrav& T, ShadowStack& K, const SceneK& S, ShadowSet* sh,
+                      const Spill& sp, Counters* cnt) {
+    int ref = T.ref;
+    uint32_t rays = T.rays;
+    while (ref >= 0) {
+        const CNode C = S.cnode[ref];
+        uint32_t m0 = 0, m1 = 0;
+        float d0 = INFINITY, d1 = INFINITY;
+#pragma unroll
+        for (int k = 0; k < kLightSamples; ++k) {
+            if (!((rays >> k) & 1u)) continue;
+            const float e0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv[k], sh->hhi[k]);
+            const float e1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv[k], sh->hhi[k]);
+            m0 |= e0 < INFINITY ? 1u << k : 0u;
+            m1 |= e1 < INFINITY ? 1u << k : 0u;
+            d0 = fminf(d0, e0);
+            d1 = fminf(d1, e1);
         }
-        if (ref == kNoRef) break;
+        const bool near0 = d0 <= d1;
+        const uint32_t mn = near0 ? m0 : m1, mf = near0 ? m1 : m0;
+        const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
+        if (mf) {
+            if (T.tc != 0) K.e[T.top++] = T.tc;
+            T.tc = (int)(((uint32_t)rf << 3) | mf);
+        }
+        if (mn) {
+            ref = rn;
+            rays = mn;
+        } else {
+            ref = strav_pop<COUNT>(T, K, S, sh);
+            rays = T.rays;
+        }
+    }
+    if (ref != kNoRef) {
         const int code = ~ref, u0 = code >> 3, nu = code & 7;
         for (int i = 0; i < nu; ++i) {
             const UnitF U = S.bunit[u0 + i];
-            fused_unit<false, COUNT>(S, U, origin_u(U, o32), U.grp == ogrp, true, false, sh,
+            fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, true, false, sh,
                                      F3{0.f, 0.f, 0.f}, nullptr, sp, cnt, rays);
         }
-        ref = pop();
+        ref = strav_pop<COUNT>(T, K, S, sh);
+        rays = T.rays;
+    }
+    T.ref = ref;
+    T.rays = rays;
+    return ref == kNoRef;
+}
+// one node or one leaf unit per call (see ctrav_step1)
+template <bool COUNT>
+PT_HD bool strav_step1(ShadowTrav& T, ShadowStack& K, const SceneK& S, ShadowSet* sh,
+                       const Spill& sp, Counters* cnt) {
+    if (T.lu < T.le) {   // one unit of the open leaf
+        const UnitF U = S.bunit[T.lu];
+        ++T.lu;
+        fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, true, false, sh,
+                                 F3{0.f, 0.f, 0.f}, nullptr, sp, cnt, T.rays);
+        if (T.lu == T.le) T.ref = strav_pop<COUNT>(T, K, S, sh);
+    } else if (T.ref >= 0) {   // one internal node
+        const CNode C = S.cnode[T.ref];
+        uint32_t m0 = 0, m1 = 0;
+        float d0 = INFINITY, d1 = INFINITY;
+#pragma unroll
+        for (int k = 0; k < kLightSamples; ++k) {
+            if (!((T.rays >> k) & 1u)) continue;
+            const float e0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv[k], sh->hhi[k]);
+            const float e1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv[k], sh->hhi[k]);
+            m0 |= e0 < INFINITY ? 1u << k : 0u;
+            m1 |= e1 < INFINITY ? 1u << k : 0u;
+            d0 = fminf(d0, e0);
+            d1 = fminf(d1, e1);
+        }
+        const bool near0 = d0 <= d1;
+        const uint32_t mn = near0 ? m0 : m1, mf = near0 ? m1 : m0;
+        const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
+        if (mf) {
+            if (T.tc != 0) K.e[T.top++] = T.tc;
+            T.tc = (int)(((uint32_t)rf << 3) | mf);
+        }
+        if (mn) {
+            T.ref = rn;
+            T.rays = mn;
+        } else {
+            T.ref = strav_pop<COUNT>(T, K, S, sh);
+        }
+    }
+    if (T.lu >= T.le && T.ref <= -2) {   // arrived at a leaf: open it
+        const int code = ~T.ref;
+        T.lu = code >> 3;
+        T.le = T.lu + (code & 7);
+        T.ref = kNoRef;
+    }
+    return T.lu >= T.le && T.ref == kNoRef;
+}
+template <bool COUNT>
+PT_HD void bvh_shadow(const SceneK& S, F3 o32, int ogrp, ShadowSet* sh, const Spill& sp,
+                      Counters* cnt) {
+    ShadowTrav T;
+    ShadowStack K;
+    strav_init<COUNT>(T, S, o32, ogrp, sh);
+    while (!strav_step<COUNT>(T, K, S, sh, sp, cnt)) {
     }
 }
 
@@ -875,7 +1041,9 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         if (BVH && S.n_bnode) {   // the meshes: shadows as a packet, the closest ray ordered
             const bool ordered = !FORCE64 && S.bvh_depth < kBvhStack;
             if (ordered) {
+#ifndef PT_ABL_NOBVHSHADOW
                 bvh_shadow<COUNT>(S, o32, ogrp, &sh, sp, cnt);
+#endif
                 if (trace) bvh_closest<COUNT>(S, o32, ogrp, n32, &ca, sp, cnt);
             } else {
                 bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, !FORCE64 && trace, &sh, n32, &ca, sp,

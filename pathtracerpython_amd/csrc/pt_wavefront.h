@@ -1,0 +1,292 @@
+// pt_wavefront.h — the wavefront form of the render loop for scenes with a
+// BVH (large meshes, BASELINE config K5).
+//
+// Why: in the single kernel (k_render) each lane runs its own BVH walks
+// (bvh_shadow, bvh_closest) inside the bounce loop.  Walk lengths vary by
+// orders of magnitude (an occluded shadow ray ends after a few nodes, an
+// unoccluded one crosses the whole mesh), so a wave waits for its longest
+// walk: measured VALU lane utilisation 9.7% on K5 (80% on the Cornell box).
+// Here the bounce loop of main.py:186-271 is cut at the walks:
+//
+//   shade    (one work-item per path slot): finish the previous bounce with
+//            the walks' results (colour, main.py:208-231; next hit,
+//            main.py:197-205), then start the next bounce — RNG, light
+//            samples, next ray (main.py:236-268), the fused pass over the
+//            uniform units — and append the slot to the shadow / closest
+//            query lists;
+//   shadow   (persistent, dynamic fetch): the BVH shadow walks;
+//   closest  (persistent, dynamic fetch): the BVH closest-hit walks.
+//
+// A query work-item takes the next query from its list (one atomic per wave)
+// as soon as its walk ends, so the waves stay full until the list drains.
+// The per-slot arithmetic is that of render_lane (pt_path.h) in the same
+// order, so the framebuffer is bitwise identical to k_render's (tested).
+// Path state lives in HBM between the kernels: WfPath (256 B per slot, the
+// f64 spill home included) and the query records.
+#pragma once
+#include "pt_path.h"
+
+namespace pt {
+
+enum : int32_t { kWfDone = 0, kWfPrimary = 1, kWfBounce = 2 };
+
+struct alignas(16) WfPath {
+    double sp[kSpillSlots];   // the spill home of pt_path.h (Spill{sp, 1})
+    double acc[3];            // sum of this slot's sample colours
+    double k, kk;             // throughput before / after the pending bounce
+    double ln[kLightSamples]; // l_k . n of the pending bounce's light samples
+    int32_t state, si, b, tri;
+    int32_t tri0, obj, trace, pad;
+};
+static_assert(sizeof(WfPath) == 256, "WfPath is 256 B");
+
+// shadow walk: in = the state after the uniform units, out = the final state
+struct alignas(16) WfShadowQ {
+    float o[3];
+    int32_t ogrp;
+    float d[kLightSamples][3];
+    float hlo[kLightSamples], hhi[kLightSamples];
+    int32_t occ;              // bit k: shadow ray k occluded
+    int32_t key2, leak;
+    int32_t pad[2];
+};
+static_assert(sizeof(WfShadowQ) == 96, "WfShadowQ is 96 B");
+
+// closest walk: in = the candidates of the uniform units, out = all candidates
+struct alignas(16) WfClosestQ {
+    float o[3];
+    int32_t ogrp;
+    float d[3];
+    int32_t i1;
+    float a1, a2, b1;
+    int32_t pad;
+};
+static_assert(sizeof(WfClosestQ) == 48, "WfClosestQ is 48 B");
+
+PT_HD void wf_put_shadow(WfShadowQ* q, F3 o32, int ogrp, const ShadowSet& sh) {
+    q->o[0] = o32.x; q->o[1] = o32.y; q->o[2] = o32.z;
+    q->ogrp = ogrp;
+    int occ = 0;
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        q->d[k][0] = sh.d32[k].x; q->d[k][1] = sh.d32[k].y; q->d[k][2] = sh.d32[k].z;
+        q->hlo[k] = sh.hlo[k];
+        q->hhi[k] = sh.hhi[k];
+        occ |= sh.occ[k] ? 1 << k : 0;
+    }
+    q->occ = occ;
+    q->key2 = sh.key2;
+    q->leak = sh.leak;
+}
+// the walk's view of a query (count-mode fields unused: the wavefront path
+// does not count)
+PT_HD void wf_get_shadow(const SceneK& S, const WfShadowQ& q, F3* o32, int* ogrp, ShadowSet* sh) {
+    *o32 = F3{q.o[0], q.o[1], q.o[2]};
+    *ogrp = q.ogrp;
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        sh->d32[k] = F3{q.d[k][0], q.d[k][1], q.d[k][2]};
+        sh->hlo[k] = q.hlo[k];
+        sh->hhi[k] = q.hhi[k];
+        sh->occ[k] = (q.occ >> k) & 1;
+        sh->first[k] = S.n_tri;
+        sh->ln[k] = 0.0;
+    }
+    sh->key2 = q.key2;
+    sh->leak = q.leak;
+}
+PT_HD void wf_put_closest(WfClosestQ* q, F3 o32, int ogrp, F3 d32, const ClosestAcc& c) {
+    q->o[0] = o32.x; q->o[1] = o32.y; q->o[2] = o32.z;
+    q->ogrp = ogrp;
+    q->d[0] = d32.x; q->d[1] = d32.y; q->d[2] = d32.z;
+    q->i1 = c.i1;
+    q->a1 = c.a1; q->a2 = c.a2; q->b1 = c.b1;
+}
+PT_HD ClosestAcc wf_get_acc(const WfClosestQ& q) {
+    ClosestAcc c;
+    c.a1 = q.a1; c.a2 = q.a2; c.b1 = q.b1; c.i1 = q.i1;
+    return c;
+}
+
+// What a shade step asks for next (bit 0: a shadow walk, bit 1: a closest walk)
+enum : uint32_t { kWfWantShadow = 1u, kWfWantClosest = 2u };
+
+// Start the slot (shade step 0): the primary ray's uniform part, as closest()
+// does for it in k_render; the BVH part is a closest query.
+PT_HD uint32_t wf_start(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfClosestQ* cq) {
+    W->acc[0] = W->acc[1] = W->acc[2] = 0.0;
+    W->state = kWfDone;
+    if (J.n_samples <= 0 || J.bounces <= 0) return 0;   // main.py:192 never runs
+    const Spill sp{W->sp, 1};
+    const D3 eye = ld3(S.eye);
+    const D3 dn = unit(d0);
+    sp.put3(kSpP, eye);
+    sp.put3(kSpNd, d0);
+    const F3 o32 = to_f3(eye - ld3(S.center));
+    const F3 d32 = to_f3(dn);
+    ClosestAcc acc = closest_init();
+    for (int u = 0; u < S.n_unit; ++u) {
+        const UnitF U = S.unit[u];
+        closest_unit<false>(S, U, origin_u(U, o32), d32, U.grp == -1, sp, kSpP, kSpNd, &acc,
+                            nullptr);
+    }
+    wf_put_closest(cq, o32, -1, d32, acc);
+    W->state = kWfPrimary;
+    return kWfWantClosest;
+}
+
+// The body of render_lane's loop up to its walks: RNG, light samples, next
+// ray, the fused pass over the uniform units (pt_path.h render_lane).
+PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfShadowQ* shq,
+                               WfClosestQ* cq) {
+    const Spill sp{W->sp, 1};
+    const D3 P = sp.get3(kSpP);
+    const int tri = W->tri, b = W->b;
+    const uint32_t sample = (uint32_t)(J.sample0 + W->si * J.sample_stride);
+    const int obj = S.tri_obj[tri];
+    const TriS R = S.tris[tri];
+    const Mat& m = S.mat[obj];
+    const int ogrp = S.tri_grp[tri];
+    uint32_t w[16];
+    rng_blocks4(J.seed, J.pixel, sample, (uint32_t)b, w);
+    ShadowSet sh;
+    {
+        double u12[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) u12[i] = u_of(w[i]);
+        shadow_setup<false>(S, P, ld3(R.n), u12, &sh, sp);
+    }
+    double kf;
+    const D3 nd = bounce(S, R, m, P, sp.get3(kSpNd), u_of(w[12]), u_of(w[13]), u_of(w[14]), &kf);
+    const double kn = W->k * kf;
+    bool trace = (b + 1 < J.bounces);
+    double kk = kn;
+    if (trace && J.rr_depth >= 0 && b >= J.rr_depth) {   // build extension
+        double q = fabs(kn);
+        q = q < 0.05 ? 0.05 : (q > 1.0 ? 1.0 : q);
+        if (u_of(w[15]) >= q) trace = false;
+        else kk = kn / q;
+    }
+    sp.put3(kSpNd, nd);
+    const F3 o32 = to_f3(P - ld3(S.center));
+    const F3 n32 = to_f3(unit(nd));
+    ClosestAcc ca = closest_init();
+    const bool any_trace = PT_WAVE_ANY(trace);
+    {
+        float oc[kLightSamples] = {-1.0f, -1.0f, -1.0f};
+        for (int u = 0; u < S.n_obj_unit; ++u) {
+            const UnitF U = S.unit[u];
+            const OriginU O = origin_u(U, o32);
+            const bool do_shadow = PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));
+            fused_unit<false, false, true>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
+                                           &ca, sp, nullptr, 15u, oc);
+        }
+#pragma unroll
+        for (int k = 0; k < kLightSamples; ++k) sh.occ[k] = oc[k] > 0.0f;
+    }
+    if (any_trace) {
+        for (int u = S.n_obj_unit; u < S.n_unit; ++u) {   // the light's units
+            const UnitF U = S.unit[u];
+            closest_unit<false>(S, U, origin_u(U, o32), n32, U.grp == ogrp, sp, kSpP, kSpNd, &ca,
+                                nullptr);
+        }
+    }
+    uint32_t want = 0;
+    wf_put_shadow(shq, o32, ogrp, sh);
+    if (shadow_open<false>(S, &sh)) want |= kWfWantShadow;
+    if (trace) {
+        wf_put_closest(cq, o32, ogrp, n32, ca);
+        want |= kWfWantClosest;
+    }
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) W->ln[k] = sh.ln[k];
+    W->obj = obj;
+    W->kk = kk;
+    W->trace = trace ? 1 : 0;
+    W->state = kWfBounce;
+    return want;
+}
+
+// Shade step >= 1: finish the pending work of the slot with the walks'
+// results, then start its next bounce.  Returns the queries wanted.
+PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfShadowQ* shq,
+                        WfClosestQ* cq) {
+    const Spill sp{W->sp, 1};
+    if (W->state == kWfPrimary) {   // k_render: closest(eye, d0) then render_lane's prologue
+        D3 P0 = d3(0, 0, 0);
+        const int tri0 = closest_finish<false, false, true>(S, wf_get_acc(*cq), sp.get3(kSpP),
+                                                            unit(sp.get3(kSpNd)), &P0, nullptr);
+        if (tri0 < 0 || tri0 >= S.n_obj_tri) {   // primary ray escapes or hits the light
+            const D3 v = tri0 < 0 ? d3(0, 0, 0) : ld3(S.light_rgb);
+            D3 acc = d3(0, 0, 0);
+            for (int i = 0; i < J.n_samples; ++i) acc = acc + v;
+            W->acc[0] = acc.x; W->acc[1] = acc.y; W->acc[2] = acc.z;
+            W->state = kWfDone;
+            return 0;
+        }
+        W->si = 0;
+        W->b = 0;
+        W->tri = tri0;
+        W->tri0 = tri0;
+        W->k = 1.0;
+        sp.put(kSpD0, d0.x);
+        sp.put(kSpD0 + 1, d0.y);
+        sp.put3(kSpP0, P0);
+        sp.put3(kSpP, P0);
+        sp.put3(kSpNd, d0);   // incoming direction of bounce 0 (main.py:191)
+        return wf_begin_bounce(S, J, W, shq, cq);
+    }
+    if (W->state != kWfBounce) return 0;
+    // the colour of the pending bounce (main.py:208-231)
+    ShadowSet sh;
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        sh.occ[k] = (shq->occ >> k) & 1;
+        sh.ln[k] = W->ln[k];
+        sh.first[k] = S.n_tri;
+    }
+    sh.leak = shq->leak;
+    const D3 col = shadow_color<false>(S, W->obj, sh, nullptr);
+    D3 acc = ld3(W->acc);
+    double k = W->k;
+    acc = acc + col * k;   // main.py:230-231 (k before this bounce's update)
+    k = W->kk;
+    bool done = W->trace == 0;
+    int tri = W->tri, b = W->b, si = W->si;
+    if (!done) {
+        D3 Pn;
+        const int tn = closest_finish<false, false, true>(S, wf_get_acc(*cq), sp.get3(kSpP),
+                                                         unit(sp.get3(kSpNd)), &Pn, nullptr, &sp);
+        if (tn < 0) {
+            done = true;
+        } else if (tn >= S.n_obj_tri) {   // light: main.py:214-215
+            acc = acc + ld3(S.light_rgb) * k;
+            done = true;
+        } else {
+            tri = tn;
+            ++b;
+        }
+    }
+    if (done) {
+        ++si;
+        if (si < J.n_samples) {   // next sample from the cached primary hit
+            b = 0;
+            tri = W->tri0;
+            k = 1.0;
+            sp.put3(kSpP, sp.get3(kSpP0));
+            sp.put3(kSpNd, d3(sp.get(kSpD0), sp.get(kSpD0 + 1), 0.0 - S.eye[2]));
+        }
+    }
+    W->acc[0] = acc.x; W->acc[1] = acc.y; W->acc[2] = acc.z;
+    W->k = k;
+    W->tri = tri;
+    W->b = b;
+    W->si = si;
+    if (si >= J.n_samples) {
+        W->state = kWfDone;
+        return 0;
+    }
+    return wf_begin_bounce(S, J, W, shq, cq);
+}
+
+}  // namespace pt

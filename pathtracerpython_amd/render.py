@@ -17,7 +17,7 @@ import ctypes as C
 import numpy as np
 
 from . import _native
-from ._abi import (PT_FLAG_COUNT, PT_FLAG_FORCE_F64, PT_FLAG_OUT_F64, PT_FLAG_RR, PtStats,
+from ._abi import (PT_FLAG_COUNT, PT_FLAG_FORCE_F64, PT_FLAG_MEGAKERNEL, PT_FLAG_OUT_F64, PT_FLAG_RR, PtStats,
                    band_rows, make_params)
 from .pack import pack_scene
 
@@ -40,13 +40,16 @@ class Renderer:
     # ------------------------------------------------------------ render --
     def params(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
                rr_depth=3, force_f64=False, count=False, out_f64=False, row_begin=0,
-               row_end=None, row_step=1, row_phase=0, sample_begin=0):
+               row_end=None, row_step=1, row_phase=0, sample_begin=0, megakernel=False):
+        """megakernel=True: scenes with a BVH render with the single kernel
+        instead of the wavefront kernels (the same framebuffer, bit for bit)."""
         width = int(self.scene.width if width is None else width)
         height = int(self.scene.height if height is None else height)
         seed = self.scene.seed if seed is None else seed
         seed = 0 if seed is None else int(seed)
         flags = (PT_FLAG_RR if rr else 0) | (PT_FLAG_FORCE_F64 if force_f64 else 0) | \
-            (PT_FLAG_COUNT if count else 0) | (PT_FLAG_OUT_F64 if out_f64 else 0)
+            (PT_FLAG_COUNT if count else 0) | (PT_FLAG_OUT_F64 if out_f64 else 0) | \
+            (PT_FLAG_MEGAKERNEL if megakernel else 0)
         return make_params(width, height, spp, bounces, seed, flags, rr_depth, row_begin,
                            row_end, row_step, row_phase, sample_begin)
 
@@ -65,11 +68,12 @@ class Renderer:
         return (out, st.as_dict()) if stats else out
 
     def render(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
-               rr_depth=3, force_f64=False, stats=False, out_f64=False, **band):
+               rr_depth=3, force_f64=False, stats=False, out_f64=False, megakernel=False,
+               **band):
         """Framebuffer (rows, W, 3), float32 (float64 with out_f64); rows = H
         for a full render.  stats=True also returns the work counters."""
         p = self.params(width, height, spp, bounces, seed, rr, rr_depth, force_f64,
-                        count=stats, out_f64=out_f64, **band)
+                        count=stats, out_f64=out_f64, megakernel=megakernel, **band)
         return self.render_params(p, stats=stats)
 
     def render_device(self, p, out_ptr, stream=None):

@@ -7,7 +7,7 @@ meta = {}
 for d in dirs:
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "k_render" not in r["Kernel_Name"]:
+            if os.environ.get("PMC_KERNEL", "k_render") not in r["Kernel_Name"]:
                 continue
             agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
             meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",

@@ -13,6 +13,7 @@
 #include <random>
 
 #include "../../pathtracerpython_amd/csrc/pt_path.h"
+#include "../../pathtracerpython_amd/csrc/pt_wavefront.h"
 #include "../../pathtracerpython_amd/csrc/pt_prepare.h"
 
 using namespace pt;
@@ -69,6 +70,95 @@ int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
                          c.light_hits, c.escapes, c.fallbacks, c.rescans};
         for (int i = 0; i < 8; ++i) counters[i] = v[i];
     }
+    return 0;
+}
+
+// The wavefront form of the render (pt_wavefront.h) run on the host: every
+// shade step over all slots, then every pending shadow and closest walk to
+// completion, as the GPU's shade / walk kernels do (split = 1, one slot per
+// pixel).  Must equal hc_render (force64 = 0, no counters) bit for bit.
+// steps_out (optional): shade steps that found work.
+int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, double* out,
+                        int32_t* steps_out) {
+    HostScene H;
+    if (!prepare_scene(d, &H).empty()) return -1;
+    bind_host(&H);
+    if (H.k.n_bnode == 0 || H.k.bvh_depth >= kBvhStack) return -3;
+    int32_t first, rows;
+    if (!band_layout(p, &first, &rows)) return -2;
+    const size_t n = (size_t)rows * p->width;
+    std::vector<WfPath> W(n);
+    std::vector<WfShadowQ> SQ(n);
+    std::vector<WfClosestQ> CQ(n);
+    std::vector<LaneJob> J(n);
+    std::vector<D3> D0(n);
+    for (int r = 0; r < rows; ++r) {
+        const int iy = first + r * p->row_step;
+        for (int ix = 0; ix < p->width; ++ix) {
+            const size_t i = (size_t)r * p->width + ix;
+            const D3 eye = ld3(H.k.eye);
+            const double x = linspace_at(H.k.ortho[0], H.k.ortho[2], p->width, ix);
+            const double y = linspace_at(H.k.ortho[1], H.k.ortho[3], p->height, iy);
+            D0[i] = d3(x - eye.x, y - eye.y, 0.0 - eye.z);
+            J[i].seed = p->seed;
+            J[i].pixel = (uint32_t)ix * (uint32_t)p->height + (uint32_t)iy;
+            J[i].sample0 = p->sample_begin;
+            J[i].sample_stride = 1;
+            J[i].n_samples = p->spp;
+            J[i].bounces = p->bounces;
+            J[i].rr_depth = (p->flags & PT_FLAG_RR) ? p->rr_depth : -1;
+        }
+    }
+    std::vector<uint32_t> want(n);
+    int32_t busy = 0;
+    for (int step = 0;; ++step) {
+        bool any = false;
+        for (size_t i = 0; i < n; ++i) {
+            want[i] = 0;
+            if (step == 0) want[i] = wf_start(H.k, J[i], D0[i], &W[i], &CQ[i]);
+            else if (W[i].state != kWfDone) {
+                want[i] = wf_shade(H.k, J[i], D0[i], &W[i], &SQ[i], &CQ[i]);
+                any = true;
+            }
+        }
+        if (step > 0 && !any) break;
+        ++busy;
+        for (size_t i = 0; i < n; ++i) {
+            const Spill sp{W[i].sp, 1};
+            if (want[i] & kWfWantShadow) {
+                ShadowSet sh;
+                F3 o32;
+                int ogrp;
+                wf_get_shadow(H.k, SQ[i], &o32, &ogrp, &sh);
+                ShadowTrav T;
+                ShadowStack K;
+                strav_init<false>(T, H.k, o32, ogrp, &sh);
+                while (!strav_step<false>(T, K, H.k, &sh, sp, nullptr)) {
+                }
+                int occ = 0;
+                for (int k = 0; k < kLightSamples; ++k) occ |= sh.occ[k] ? 1 << k : 0;
+                SQ[i].occ = occ;
+                SQ[i].leak = sh.leak;
+            }
+            if (want[i] & kWfWantClosest) {
+                ClosestAcc ca = wf_get_acc(CQ[i]);
+                ClosestTrav T;
+                ClosestStack K;
+                const WfClosestQ& q = CQ[i];
+                ctrav_init(T, H.k, F3{q.o[0], q.o[1], q.o[2]}, q.ogrp, F3{q.d[0], q.d[1], q.d[2]}, ca.b1);
+                while (!ctrav_step<false>(T, K, H.k, &ca, sp, nullptr)) {
+                }
+                CQ[i].a1 = ca.a1; CQ[i].a2 = ca.a2; CQ[i].b1 = ca.b1; CQ[i].i1 = ca.i1;
+            }
+        }
+    }
+    for (int r = 0; r < rows; ++r)
+        for (int ix = 0; ix < p->width; ++ix) {
+            const size_t i = (size_t)r * p->width + ix;
+            double* o = out + ((size_t)(rows - 1 - r) * p->width + ix) * 3;
+            o[0] = W[i].acc[0] / p->spp; o[1] = W[i].acc[1] / p->spp; o[2] = W[i].acc[2] / p->spp;
+        }
+    if (steps_out) *steps_out = busy;
     return 0;
 }
 

@@ -146,6 +146,42 @@ def test_random_mesh_scene(tmp_path):
         assert np.array_equal(fb, r.render(48, 48, 4, 5, 8, out_f64=True, force_f64=True))
     ref, _ = oracle.render(pk, 48, 48, 4, 5, 8)
     assert np.abs(to_list_order(fb) - ref).max() <= TOL
+    with Renderer(sc) as r:   # wavefront (default for BVH scenes) == single kernel
+        assert np.array_equal(fb, r.render(48, 48, 4, 5, 8, out_f64=True, megakernel=True))
+
+
+@pytest.fixture(scope="module")
+def k5small(tmp_path_factory):
+    """The K5 recipe (synth.py) with 20k triangles: a BVH scene."""
+    from pathtracerpython_amd import scene_reader
+    from pathtracerpython_amd.synth import write_k5_scene
+    scene_reader.VERBOSE = False
+    d = tmp_path_factory.mktemp("k5")
+    return scene_reader.Scene(write_k5_scene(str(d), n_tris=20_000, seed=0, size=64))
+
+
+@pytest.mark.parametrize("W,spp,B,rr", [(64, 4, 4, False), (48, 3, 6, True), (40, 1, 1, False),
+                                        (100, 2, 3, False)])
+def test_wavefront_k5_equals_single_kernel(k5small, W, spp, B, rr):
+    """BVH scenes render through the wavefront kernels (shade + persistent
+    walk kernels); the framebuffer must equal the single kernel's bit for bit
+    (which equals the forced-f64 render), and the oracle to rounding."""
+    pk = pack_scene(k5small)
+    with Renderer(k5small) as r:
+        wf = r.render(W, W, spp, B, 9, rr=rr, out_f64=True)
+        mk = r.render(W, W, spp, B, 9, rr=rr, out_f64=True, megakernel=True)
+        assert np.array_equal(wf, mk)
+        if W <= 48:
+            assert np.array_equal(wf, r.render(W, W, spp, B, 9, rr=rr, out_f64=True,
+                                               force_f64=True))
+        # a band and a sample slice of the same image (kernel reuse, odd sizes)
+        band = r.render(W, W, spp, B, 9, rr=rr, out_f64=True, row_begin=7, row_end=W - 3)
+        assert np.array_equal(band, wf[3:W - 7])
+    rows = [0, W // 2, W - 1]
+    pix = np.array([ix * W + iy for iy in rows for ix in range(0, W, 3)], dtype=np.int64)
+    ref, _ = oracle.render(pk, W, W, spp, B, 9, flags=1 if rr else 0, pixels=pix)
+    got = np.array([wf[W - 1 - (k % W), k // W] for k in pix])
+    assert np.abs(got - ref).max() <= TOL
 
 
 # ------------------------------------------- batched Pool callables --
