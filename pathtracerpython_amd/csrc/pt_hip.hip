@@ -224,16 +224,24 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
 }
 
 // Persistent walk kernels: a work-item holds one query at a time and takes
-// the next one from the list as soon as its walk ends.
+// the next one from the list as soon as its walk ends.  A loop turn is one
+// "while-while" round, except that the node phase ends for the whole wave
+// once at most `thr` of its lanes are still descending and some lane has a
+// leaf to test (the others carry on in the next turn): the wave does not wait
+// for its longest node run, and lanes whose walk ended are refilled every
+// turn.  Every turn makes progress (a node step, a leaf or a fetch), and a
+// lane whose list is exhausted stays idle, so the loop drains.
 __global__ __launch_bounds__(256) void k_wf_shadow(SceneK S, WfPath* __restrict__ W,
                                                    WfShadowQ* __restrict__ SQ,
-                                                   const int32_t* __restrict__ list, int32_t* counters) {
+                                                   const int32_t* __restrict__ list, int32_t* counters,
+                                                   int32_t thr) {
     const int32_t count = counters[0];
     int32_t slot = -1;
     bool exhausted = false;
     ShadowSet sh;
     ShadowTrav T;
     ShadowStack K;
+    T.ref = kNoRef;
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
@@ -251,29 +259,36 @@ __global__ __launch_bounds__(256) void k_wf_shadow(SceneK S, WfPath* __restrict_
             }
         }
         if (__all(slot < 0)) break;
-        if (slot >= 0) {
-            const Spill sp{W[slot].sp, 1};
-            if (strav_step<false>(T, K, S, &sh, sp, nullptr)) {
-                int occ = 0;
+        while (true) {   // node phase (wave-uniform loop)
+            const bool desc = slot >= 0 && T.ref >= 0;
+            const int32_t nd = (int32_t)__popcll(__ballot(desc));
+            // end it early only when some lane has a leaf to test (progress)
+            if (nd == 0 || (nd <= thr && __any(slot >= 0 && T.ref <= -2))) break;
+            if (desc) strav_node<false>(T, K, S, &sh);
+        }
+        if (slot >= 0 && T.ref <= -2) strav_leaf<false>(T, K, S, &sh, Spill{W[slot].sp, 1}, nullptr);
+        if (slot >= 0 && T.ref == kNoRef) {
+            int occ = 0;
 #pragma unroll
-                for (int k = 0; k < kLightSamples; ++k) occ |= sh.occ[k] ? 1 << k : 0;
-                SQ[slot].occ = occ;
-                SQ[slot].leak = sh.leak;
-                slot = -1;
-            }
+            for (int k = 0; k < kLightSamples; ++k) occ |= sh.occ[k] ? 1 << k : 0;
+            SQ[slot].occ = occ;
+            SQ[slot].leak = sh.leak;
+            slot = -1;
         }
     }
 }
 
 __global__ __launch_bounds__(256) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
                                                     WfClosestQ* __restrict__ CQ,
-                                                    const int32_t* __restrict__ list, int32_t* counters) {
+                                                    const int32_t* __restrict__ list, int32_t* counters,
+                                                    int32_t thr) {
     const int32_t count = counters[2];
     int32_t slot = -1;
     bool exhausted = false;
     ClosestAcc ca = closest_init();
     ClosestTrav T;
     ClosestStack K;
+    T.ref = kNoRef;
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
@@ -291,15 +306,20 @@ __global__ __launch_bounds__(256) void k_wf_closest(SceneK S, WfPath* __restrict
             }
         }
         if (__all(slot < 0)) break;
-        if (slot >= 0) {
-            const Spill sp{W[slot].sp, 1};
-            if (ctrav_step<false>(T, K, S, &ca, sp, nullptr)) {
-                CQ[slot].a1 = ca.a1;
-                CQ[slot].a2 = ca.a2;
-                CQ[slot].b1 = ca.b1;
-                CQ[slot].i1 = ca.i1;
-                slot = -1;
-            }
+        while (true) {   // node phase (wave-uniform loop)
+            const bool desc = slot >= 0 && T.ref >= 0;
+            const int32_t nd = (int32_t)__popcll(__ballot(desc));
+            // end it early only when some lane has a leaf to test (progress)
+            if (nd == 0 || (nd <= thr && __any(slot >= 0 && T.ref <= -2))) break;
+            if (desc) ctrav_node(T, K, S, &ca);
+        }
+        if (slot >= 0 && T.ref <= -2) ctrav_leaf<false>(T, K, S, &ca, Spill{W[slot].sp, 1}, nullptr);
+        if (slot >= 0 && T.ref == kNoRef) {
+            CQ[slot].a1 = ca.a1;
+            CQ[slot].a2 = ca.a2;
+            CQ[slot].b1 = ca.b1;
+            CQ[slot].i1 = ca.i1;
+            slot = -1;
         }
     }
 }
@@ -531,6 +551,16 @@ static uint32_t choose_split(uint32_t npix, int32_t spp) {
     return s;
 }
 
+// node-phase exit threshold of the walk kernels (lanes still descending);
+// PT_WF_THR overrides it for tuning sweeps
+static int32_t wf_thr() {
+    static const int32_t v = [] {
+        const char* e = getenv("PT_WF_THR");
+        return e ? (int32_t)strtol(e, nullptr, 10) : 4;
+    }();
+    return v;
+}
+
 // The wavefront render of a BVH scene (pt_wavefront.h): per step one shade
 // launch over the path slots, then the two persistent walk launches over the
 // queries it appended.  A slot runs at most n_samples x bounces bounces plus
@@ -567,9 +597,9 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
                            counters, (uint32_t)slots);
         if (step + 1 < steps) {
             hipLaunchKernelGGL(k_wf_shadow, dim3(walk_blocks), dim3(256), 0, st, s->dev, W, SQ,
-                               (const int32_t*)lists, counters);
+                               (const int32_t*)lists, counters, wf_thr());
             hipLaunchKernelGGL(k_wf_closest, dim3(walk_blocks), dim3(256), 0, st, s->dev, W, CQ,
-                               (const int32_t*)(lists + slots), counters);
+                               (const int32_t*)(lists + slots), counters, wf_thr());
         }
     }
     hipLaunchKernelGGL(k_wf_final, grid, dim3(256), 0, st, s->dev, R, (const WfPath*)W, out_dev);

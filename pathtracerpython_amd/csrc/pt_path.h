@@ -588,8 +588,7 @@ PT_HD float cbox_dist(const float* lo, const float* hi, F3 o32, F3 inv, float R)
 struct ClosestTrav {
     F3 o32, d32, inv;
     int ogrp;
-    int ref;                  // next node / leaf (kNoRef: done)
-    int lu, le;               // ctrav_step1: units [lu, le) of the open leaf
+    int ref;                  // next node / leaf (<= -2: leaf code; kNoRef: done)
     int top;                  // entries in the scratch part
     int tref;                 // cached top (kNoRef: empty)
     float tdist;
@@ -625,65 +624,38 @@ PT_HD void ctrav_init(ClosestTrav& T, const SceneK& S, F3 o32, int ogrp, F3 d32,
     T.tref = kNoRef;
     T.tdist = INFINITY;
     T.ref = node_dist(S, 0, o32, T.inv, bound) < INFINITY ? S.bvh_root : kNoRef;
-    T.lu = T.le = 0;
 }
-// one round; returns true when the traversal has ended
+// one internal node (T.ref >= 0): nearer child next, the farther stacked
+PT_HD void ctrav_node(ClosestTrav& T, ClosestStack& K, const SceneK& S, const ClosestAcc* ca) {
+    const CNode C = S.cnode[T.ref];
+    const float d0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv, ca->b1);
+    const float d1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv, ca->b1);
+    const bool near0 = d0 <= d1;
+    const float dn = near0 ? d0 : d1, df = near0 ? d1 : d0;
+    const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
+    if (df < INFINITY) ctrav_push(T, K, rf, df);
+    T.ref = dn < INFINITY ? rn : ctrav_pop(T, K, ca->b1);
+}
+// the leaf T.ref (<= -2: leaf codes have a unit count >= 1), then the next entry
+template <bool COUNT>
+PT_HD void ctrav_leaf(ClosestTrav& T, ClosestStack& K, const SceneK& S, ClosestAcc* ca,
+                      const Spill& sp, Counters* cnt) {
+    const int code = ~T.ref, u0 = code >> 3, nu = code & 7;
+    for (int i = 0; i < nu; ++i) {
+        const UnitF U = S.bunit[u0 + i];
+        fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, false, true, nullptr,
+                                 T.d32, ca, sp, cnt, 8u);
+    }
+    T.ref = ctrav_pop(T, K, ca->b1);
+}
+// one "while-while" round: walk internal nodes to the next leaf, test it;
+// returns true when the traversal has ended
 template <bool COUNT>
 PT_HD bool ctrav_step(ClosestTrav& T, ClosestStack& K, const SceneK& S, ClosestAcc* ca,
                       const Spill& sp, Counters* cnt) {
-    int ref = T.ref;
-    while (ref >= 0) {   // "while-while": descend to a leaf, then test leaves together
-        const CNode C = S.cnode[ref];
-        const float d0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv, ca->b1);
-        const float d1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv, ca->b1);
-        const bool near0 = d0 <= d1;
-        const float dn = near0 ? d0 : d1, df = near0 ? d1 : d0;
-        const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
-        if (df < INFINITY) ctrav_push(T, K, rf, df);
-        ref = dn < INFINITY ? rn : ctrav_pop(T, K, ca->b1);
-    }
-    if (ref != kNoRef) {
-        const int code = ~ref, u0 = code >> 3, nu = code & 7;
-        for (int i = 0; i < nu; ++i) {
-            const UnitF U = S.bunit[u0 + i];
-            fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, false, true, nullptr,
-                                     T.d32, ca, sp, cnt, 8u);
-        }
-        ref = ctrav_pop(T, K, ca->b1);
-    }
-    T.ref = ref;
-    return ref == kNoRef;
-}
-// The same walk in quanta of one node or one leaf unit ("if-if"): the
-// wavefront walk kernels call it once per loop turn, so every turn costs the
-// same and a lane whose walk ends is refilled at the next turn.  Leaf refs
-// are <= -2 (leaf codes have a unit count >= 1).
-template <bool COUNT>
-PT_HD bool ctrav_step1(ClosestTrav& T, ClosestStack& K, const SceneK& S, ClosestAcc* ca,
-                       const Spill& sp, Counters* cnt) {
-    if (T.lu < T.le) {   // one unit of the open leaf
-        const UnitF U = S.bunit[T.lu];
-        ++T.lu;
-        fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, false, true, nullptr,
-                                 T.d32, ca, sp, cnt, 8u);
-        if (T.lu == T.le) T.ref = ctrav_pop(T, K, ca->b1);
-    } else if (T.ref >= 0) {   // one internal node
-        const CNode C = S.cnode[T.ref];
-        const float d0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv, ca->b1);
-        const float d1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv, ca->b1);
-        const bool near0 = d0 <= d1;
-        const float dn = near0 ? d0 : d1, df = near0 ? d1 : d0;
-        const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
-        if (df < INFINITY) ctrav_push(T, K, rf, df);
-        T.ref = dn < INFINITY ? rn : ctrav_pop(T, K, ca->b1);
-    }
-    if (T.lu >= T.le && T.ref <= -2) {   // arrived at a leaf: open it
-        const int code = ~T.ref;
-        T.lu = code >> 3;
-        T.le = T.lu + (code & 7);
-        T.ref = kNoRef;
-    }
-    return T.lu >= T.le && T.ref == kNoRef;
+    while (T.ref >= 0) ctrav_node(T, K, S, ca);
+    if (T.ref != kNoRef) ctrav_leaf<COUNT>(T, K, S, ca, sp, cnt);
+    return T.ref == kNoRef;
 }
 template <bool COUNT>
 PT_HD void bvh_closest(const SceneK& S, F3 o32, int ogrp, F3 d32, ClosestAcc* ca, const Spill& sp,
@@ -706,7 +678,6 @@ struct ShadowTrav {
     int ogrp;
     int ref;                  // next node / leaf (kNoRef: done)
     uint32_t rays;            // the lines that entered ref's box
-    int lu, le;               // strav_step1: units [lu, le) of the open leaf
     int top;
     int tc;                   // cached top entry (0: empty; a real entry has a ray bit)
 };
@@ -742,101 +713,57 @@ PT_HD void strav_init(ShadowTrav& T, const SceneK& S, F3 o32, int ogrp, const Sh
         if (((open >> k) & 1u) && box_hit(l, h, T.inv[k], sh->hhi[k])) rays |= 1u << k;
     T.rays = rays;
     T.ref = rays ? S.bvh_root : kNoRef;
-    T.lu = T.le = 0;
 }
+// one internal node (T.ref >= 0): the nearer child (by the smallest |t| of
+// its rays) next, the farther stacked with its rays
+template <bool COUNT>
+PT_HD void strav_node(ShadowTrav& T, ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
+    const CNode C = S.cnode[T.ref];
+    uint32_t m0 = 0, m1 = 0;
+    float d0 = INFINITY, d1 = INFINITY;
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        if (!((T.rays >> k) & 1u)) continue;
+        const float e0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv[k], sh->hhi[k]);
+        const float e1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv[k], sh->hhi[k]);
+        m0 |= e0 < INFINITY ? 1u << k : 0u;
+        m1 |= e1 < INFINITY ? 1u << k : 0u;
+        d0 = fminf(d0, e0);
+        d1 = fminf(d1, e1);
+    }
+    const bool near0 = d0 <= d1;
+    const uint32_t mn = near0 ? m0 : m1, mf = near0 ? m1 : m0;
+    const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
+    if (mf) {
+        if (T.tc != 0) K.e[T.top++] = T.tc;
+        T.tc = (int)(((uint32_t)rf << 3) | mf);
+    }
+    if (mn) {
+        T.ref = rn;
+        T.rays = mn;
+    } else {
+        T.ref = strav_pop<COUNT>(T, K, S, sh);
+    }
+}
+// the leaf T.ref (<= -2) with the rays that reached it, then the next entry
+template <bool COUNT>
+PT_HD void strav_leaf(ShadowTrav& T, ShadowStack& K, const SceneK& S, ShadowSet* sh,
+                      const Spill& sp, Counters* cnt) {
+    const int code = ~T.ref, u0 = code >> 3, nu = code & 7;
+    for (int i = 0; i < nu; ++i) {
+        const UnitF U = S.bunit[u0 + i];
+        fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, true, false, sh,
+                                 F3{0.f, 0.f, 0.f}, nullptr, sp, cnt, T.rays);
+    }
+    T.ref = strav_pop<COUNT>(T, K, S, sh);
+}
+// one "while-while" round; returns true when the traversal has ended
 template <bool COUNT>
 PT_HD bool strav_step(ShadowTrav& T, ShadowStack& K, const SceneK& S, ShadowSet* sh,
                       const Spill& sp, Counters* cnt) {
-    int ref = T.ref;
-    uint32_t rays = T.rays;
-    while (ref >= 0) {
-        const CNode C = S.cnode[ref];
-        uint32_t m0 = 0, m1 = 0;
-        float d0 = INFINITY, d1 = INFINITY;
-#pragma unroll
-        for (int k = 0; k < kLightSamples; ++k) {
-            if (!((rays >> k) & 1u)) continue;
-            const float e0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv[k], sh->hhi[k]);
-            const float e1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv[k], sh->hhi[k]);
-            m0 |= e0 < INFINITY ? 1u << k : 0u;
-            m1 |= e1 < INFINITY ? 1u << k : 0u;
-            d0 = fminf(d0, e0);
-            d1 = fminf(d1, e1);
-        }
-        const bool near0 = d0 <= d1;
-        const uint32_t mn = near0 ? m0 : m1, mf = near0 ? m1 : m0;
-        const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
-        if (mf) {
-            if (T.tc != 0) K.e[T.top++] = T.tc;
-            T.tc = (int)(((uint32_t)rf << 3) | mf);
-        }
-        if (mn) {
-            ref = rn;
-            rays = mn;
-        } else {
-            ref = strav_pop<COUNT>(T, K, S, sh);
-            rays = T.rays;
-        }
-    }
-    if (ref != kNoRef) {
-        const int code = ~ref, u0 = code >> 3, nu = code & 7;
-        for (int i = 0; i < nu; ++i) {
-            const UnitF U = S.bunit[u0 + i];
-            fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, true, false, sh,
-                                     F3{0.f, 0.f, 0.f}, nullptr, sp, cnt, rays);
-        }
-        ref = strav_pop<COUNT>(T, K, S, sh);
-        rays = T.rays;
-    }
-    T.ref = ref;
-    T.rays = rays;
-    return ref == kNoRef;
-}
-// one node or one leaf unit per call (see ctrav_step1)
-template <bool COUNT>
-PT_HD bool strav_step1(ShadowTrav& T, ShadowStack& K, const SceneK& S, ShadowSet* sh,
-                       const Spill& sp, Counters* cnt) {
-    if (T.lu < T.le) {   // one unit of the open leaf
-        const UnitF U = S.bunit[T.lu];
-        ++T.lu;
-        fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, true, false, sh,
-                                 F3{0.f, 0.f, 0.f}, nullptr, sp, cnt, T.rays);
-        if (T.lu == T.le) T.ref = strav_pop<COUNT>(T, K, S, sh);
-    } else if (T.ref >= 0) {   // one internal node
-        const CNode C = S.cnode[T.ref];
-        uint32_t m0 = 0, m1 = 0;
-        float d0 = INFINITY, d1 = INFINITY;
-#pragma unroll
-        for (int k = 0; k < kLightSamples; ++k) {
-            if (!((T.rays >> k) & 1u)) continue;
-            const float e0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv[k], sh->hhi[k]);
-            const float e1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv[k], sh->hhi[k]);
-            m0 |= e0 < INFINITY ? 1u << k : 0u;
-            m1 |= e1 < INFINITY ? 1u << k : 0u;
-            d0 = fminf(d0, e0);
-            d1 = fminf(d1, e1);
-        }
-        const bool near0 = d0 <= d1;
-        const uint32_t mn = near0 ? m0 : m1, mf = near0 ? m1 : m0;
-        const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
-        if (mf) {
-            if (T.tc != 0) K.e[T.top++] = T.tc;
-            T.tc = (int)(((uint32_t)rf << 3) | mf);
-        }
-        if (mn) {
-            T.ref = rn;
-            T.rays = mn;
-        } else {
-            T.ref = strav_pop<COUNT>(T, K, S, sh);
-        }
-    }
-    if (T.lu >= T.le && T.ref <= -2) {   // arrived at a leaf: open it
-        const int code = ~T.ref;
-        T.lu = code >> 3;
-        T.le = T.lu + (code & 7);
-        T.ref = kNoRef;
-    }
-    return T.lu >= T.le && T.ref == kNoRef;
+    while (T.ref >= 0) strav_node<COUNT>(T, K, S, sh);
+    if (T.ref != kNoRef) strav_leaf<COUNT>(T, K, S, sh, sp, cnt);
+    return T.ref == kNoRef;
 }
 template <bool COUNT>
 PT_HD void bvh_shadow(const SceneK& S, F3 o32, int ogrp, ShadowSet* sh, const Spill& sp,

@@ -78,8 +78,11 @@ int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
 // completion, as the GPU's shade / walk kernels do (split = 1, one slot per
 // pixel).  Must equal hc_render (force64 = 0, no counters) bit for bit.
 // steps_out (optional): shade steps that found work.
+// walk_stats (optional, int64[8]): shadow queries, node visits, leaves,
+// leaf units; the same for the closest walks.
 int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, double* out,
-                        int32_t* steps_out) {
+                        int32_t* steps_out, int64_t* walk_stats) {
+    int64_t ws[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HostScene H;
     if (!prepare_scene(d, &H).empty()) return -1;
     bind_host(&H);
@@ -133,7 +136,14 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
                 ShadowTrav T;
                 ShadowStack K;
                 strav_init<false>(T, H.k, o32, ogrp, &sh);
-                while (!strav_step<false>(T, K, H.k, &sh, sp, nullptr)) {
+                ++ws[0];
+                while (T.ref != kNoRef) {   // strav_step, counted
+                    while (T.ref >= 0) { strav_node<false>(T, K, H.k, &sh); ++ws[1]; }
+                    if (T.ref != kNoRef) {
+                        ++ws[2];
+                        ws[3] += (~T.ref) & 7;
+                        strav_leaf<false>(T, K, H.k, &sh, sp, nullptr);
+                    }
                 }
                 int occ = 0;
                 for (int k = 0; k < kLightSamples; ++k) occ |= sh.occ[k] ? 1 << k : 0;
@@ -146,7 +156,14 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
                 ClosestStack K;
                 const WfClosestQ& q = CQ[i];
                 ctrav_init(T, H.k, F3{q.o[0], q.o[1], q.o[2]}, q.ogrp, F3{q.d[0], q.d[1], q.d[2]}, ca.b1);
-                while (!ctrav_step<false>(T, K, H.k, &ca, sp, nullptr)) {
+                ++ws[4];
+                while (T.ref != kNoRef) {   // ctrav_step, counted
+                    while (T.ref >= 0) { ctrav_node(T, K, H.k, &ca); ++ws[5]; }
+                    if (T.ref != kNoRef) {
+                        ++ws[6];
+                        ws[7] += (~T.ref) & 7;
+                        ctrav_leaf<false>(T, K, H.k, &ca, sp, nullptr);
+                    }
                 }
                 CQ[i].a1 = ca.a1; CQ[i].a2 = ca.a2; CQ[i].b1 = ca.b1; CQ[i].i1 = ca.i1;
             }
@@ -159,6 +176,7 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
             o[0] = W[i].acc[0] / p->spp; o[1] = W[i].acc[1] / p->spp; o[2] = W[i].acc[2] / p->spp;
         }
     if (steps_out) *steps_out = busy;
+    if (walk_stats) memcpy(walk_stats, ws, sizeof(ws));
     return 0;
 }
 

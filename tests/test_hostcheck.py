@@ -187,7 +187,8 @@ def _wavefront_case(hostcheck, pk, W, H, spp, B, seed, flags=0):
     out = np.zeros((H, W, 3))
     steps = C.c_int32(0)
     rc = hostcheck.hc_render_wavefront(C.byref(pk.desc), C.byref(p),
-                                       out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(steps))
+                                       out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(steps),
+                                       None)
     assert rc == 0
     assert np.array_equal(out, ref)
     assert 1 <= steps.value <= spp * B + 2   # start, one per bounce, the last finish
@@ -216,4 +217,5 @@ def test_wavefront_needs_a_bvh(hostcheck, packed):
     p = make_params(8, 8, 1, 2, 1)
     out = np.zeros((8, 8, 3))
     assert hostcheck.hc_render_wavefront(C.byref(packed.desc), C.byref(p),
-                                         out.ctypes.data_as(C.POINTER(C.c_double)), None) == -3
+                                         out.ctypes.data_as(C.POINTER(C.c_double)), None,
+                                         None) == -3
