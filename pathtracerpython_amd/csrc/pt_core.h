@@ -126,6 +126,22 @@ struct alignas(16) CNode {
 };
 constexpr int32_t kNoRef = -1;
 
+// The wavefront walks' node form: 4 children per 64-B node, child boxes
+// quantised to 8 bits on a per-node grid (after Ylitie, Karras & Laine 2017,
+// "Efficient incoherent ray traversal on GPUs through compressed wide BVHs").
+// Grid steps are powers of two and the host checks that every decoded bound
+// org + q * step is an f32 value (pt_prepare.h build_qnodes), so the kernel's
+// fmaf decode is exact and the decoded box contains the child's (already
+// conservatively inflated) box: pruning stays conservative.
+struct alignas(16) QNode {
+    float org[3];
+    uint32_t ex;               // byte a: biased f32 exponent of axis a's grid step
+    uint32_t qlo[3], qhi[3];   // axis a, byte c: child c's bounds in grid steps
+    int32_t ref[4];            // >= 0 QNode, <= -2 leaf (~code), kNoRef: no child
+    int32_t pad[2];
+};
+static_assert(sizeof(QNode) == 64, "QNode is 64 B");
+
 struct SceneK {
     const UnitF* unit;          // [n_unit] uniform plane units: object units (small objects, scene
                                 // order), then the light's; large meshes go to the BVH
@@ -151,6 +167,9 @@ struct SceneK {
     int32_t bvh_root;            // the root as a CNode reference (0, or ~code for a leaf root)
     int32_t pad3[2];
     const CNode* cnode;          // [n_bnode - leaves] the two-child form of bnode
+    const QNode* qnode;          // [n_qnode] the 4-wide quantised form (wavefront walks)
+    int32_t n_qnode, qroot;      // qroot: a QNode, or ~code for a leaf root
+    int32_t qstack, pad4;        // stack entries a 4-wide walk can need
 };
 
 // ------------------------------------------------------------------ RNG --

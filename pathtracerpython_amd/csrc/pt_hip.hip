@@ -175,6 +175,7 @@ __global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __
 // ------------------------------------------------- wavefront (BVH scenes) --
 // pt_wavefront.h.  Queue counters: [0] shadow count, [1] shadow head,
 // [2] closest count, [3] closest head; lists[0..slots) shadow, then closest.
+// A walk kernel gets its list and its [count, head] pair.
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
@@ -223,15 +224,19 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
     wf_append((want & kWfWantClosest) != 0, &counters[2], lists + slots, (int32_t)tid);
 }
 
-// Persistent walk kernels: a work-item holds one query at a time and takes
-// the next one from the list as soon as its walk ends.  A loop turn is one
+// Persistent walk kernels over the 4-wide quantised BVH (QNode): a
+// work-item holds one query at a time and takes the next one from the list
+// as soon as its walk ends.  A loop turn is one
 // "while-while" round, except that the node phase ends for the whole wave
 // once at most `thr` of its lanes are still descending and some lane has a
 // leaf to test (the others carry on in the next turn): the wave does not wait
 // for its longest node run, and lanes whose walk ended are refilled every
 // turn.  Every turn makes progress (a node step, a leaf or a fetch), and a
 // lane whose list is exhausted stays idle, so the loop drains.
-__global__ __launch_bounds__(256) void k_wf_shadow(SceneK S, WfPath* __restrict__ W,
+#ifndef PT_WALK_WAVES
+#define PT_WALK_WAVES 1
+#endif
+__global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPath* __restrict__ W,
                                                    WfShadowQ* __restrict__ SQ,
                                                    const int32_t* __restrict__ list, int32_t* counters,
                                                    int32_t thr) {
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(256) void k_wf_shadow(SceneK S, WfPath* __restrict_
                     F3 o32;
                     int ogrp;
                     wf_get_shadow(S, SQ[slot], &o32, &ogrp, &sh);
-                    strav_init<false>(T, S, o32, ogrp, &sh);
+                    strav_init<false>(T, S, o32, ogrp, &sh, S.qroot);
                 } else {
                     exhausted = true;
                 }
@@ -264,7 +269,7 @@ __global__ __launch_bounds__(256) void k_wf_shadow(SceneK S, WfPath* __restrict_
             const int32_t nd = (int32_t)__popcll(__ballot(desc));
             // end it early only when some lane has a leaf to test (progress)
             if (nd == 0 || (nd <= thr && __any(slot >= 0 && T.ref <= -2))) break;
-            if (desc) strav_node<false>(T, K, S, &sh);
+            if (desc) strav_qnode<false>(T, K, S, &sh);
         }
         if (slot >= 0 && T.ref <= -2) strav_leaf<false>(T, K, S, &sh, Spill{W[slot].sp, 1}, nullptr);
         if (slot >= 0 && T.ref == kNoRef) {
@@ -278,11 +283,11 @@ __global__ __launch_bounds__(256) void k_wf_shadow(SceneK S, WfPath* __restrict_
     }
 }
 
-__global__ __launch_bounds__(256) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
+__global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
                                                     WfClosestQ* __restrict__ CQ,
                                                     const int32_t* __restrict__ list, int32_t* counters,
                                                     int32_t thr) {
-    const int32_t count = counters[2];
+    const int32_t count = counters[0];   // [count, head]
     int32_t slot = -1;
     bool exhausted = false;
     ClosestAcc ca = closest_init();
@@ -292,14 +297,14 @@ __global__ __launch_bounds__(256) void k_wf_closest(SceneK S, WfPath* __restrict
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
-            const int32_t i = wf_fetch(need, &counters[3]);
+            const int32_t i = wf_fetch(need, &counters[1]);
             if (need) {
                 if (i < count) {
                     slot = list[i];
                     const WfClosestQ q = CQ[slot];
                     ca = wf_get_acc(q);
                     ctrav_init(T, S, F3{q.o[0], q.o[1], q.o[2]}, q.ogrp, F3{q.d[0], q.d[1], q.d[2]},
-                               ca.b1);
+                               ca.b1, S.qroot);
                 } else {
                     exhausted = true;
                 }
@@ -311,7 +316,7 @@ __global__ __launch_bounds__(256) void k_wf_closest(SceneK S, WfPath* __restrict
             const int32_t nd = (int32_t)__popcll(__ballot(desc));
             // end it early only when some lane has a leaf to test (progress)
             if (nd == 0 || (nd <= thr && __any(slot >= 0 && T.ref <= -2))) break;
-            if (desc) ctrav_node(T, K, S, &ca);
+            if (desc) ctrav_qnode(T, K, S, &ca);
         }
         if (slot >= 0 && T.ref <= -2) ctrav_leaf<false>(T, K, S, &ca, Spill{W[slot].sp, 1}, nullptr);
         if (slot >= 0 && T.ref == kNoRef) {
@@ -473,17 +478,18 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         return fail(PT_ENODEV, "device is " + arch + ", this build targets gfx950 only");
     }
     HostScene& H = s->host;
-    constexpr int kArrays = 11;
+    constexpr int kArrays = 12;
     const size_t sz[kArrays] = {H.unit.size() * sizeof(UnitF), H.trid.size() * sizeof(TriD),
                                 H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
                                 H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
                                 H.light_cum.size() * sizeof(double),
                                 H.tri_grp.size() * sizeof(int32_t),
                                 H.bnode.size() * sizeof(BNode), H.bunit.size() * sizeof(UnitF),
-                                H.cnode.size() * sizeof(CNode)};
+                                H.cnode.size() * sizeof(CNode), H.qnode.size() * sizeof(QNode)};
     const void* src[kArrays] = {H.unit.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
                                 H.mat.data(), H.light_tri.data(), H.light_cum.data(),
-                                H.tri_grp.data(), H.bnode.data(), H.bunit.data(), H.cnode.data()};
+                                H.tri_grp.data(), H.bnode.data(), H.bunit.data(), H.cnode.data(),
+                                H.qnode.data()};
     size_t off[kArrays], total = 0;
     for (int i = 0; i < kArrays; ++i) { off[i] = total; total += align_up(sz[i]); }
     int rc = PT_OK;
@@ -509,6 +515,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     s->dev.bnode = (const BNode*)(b + off[8]);
     s->dev.bunit = (const UnitF*)(b + off[9]);
     s->dev.cnode = (const CNode*)(b + off[10]);
+    s->dev.qnode = (const QNode*)(b + off[11]);
     s->xbound = box_bound(H);
     *out = s;
     return rc;
@@ -599,7 +606,7 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
             hipLaunchKernelGGL(k_wf_shadow, dim3(walk_blocks), dim3(256), 0, st, s->dev, W, SQ,
                                (const int32_t*)lists, counters, wf_thr());
             hipLaunchKernelGGL(k_wf_closest, dim3(walk_blocks), dim3(256), 0, st, s->dev, W, CQ,
-                               (const int32_t*)(lists + slots), counters, wf_thr());
+                               (const int32_t*)(lists + slots), counters + 2, wf_thr());
         }
     }
     hipLaunchKernelGGL(k_wf_final, grid, dim3(256), 0, st, s->dev, R, (const WfPath*)W, out_dev);
@@ -639,7 +646,8 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     // for the single kernel (and for counting / forced-f64 launches, which
     // only the single kernel implements)
     const bool wavefront = s->dev.n_bnode > 0 && !count && !f64 &&
-                           !(p->flags & PT_FLAG_MEGAKERNEL) && s->dev.bvh_depth < kBvhStack;
+                           !(p->flags & PT_FLAG_MEGAKERNEL) && s->dev.n_qnode > 0 &&
+                           s->dev.qstack <= kBvhStack;
     if (wavefront) {
         rc = render_wavefront(s, R, grid, out_dev, st);
         if (!rc && stats) memset(stats, 0, sizeof(*stats));

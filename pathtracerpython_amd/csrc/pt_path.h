@@ -615,7 +615,9 @@ PT_HD int ctrav_pop(ClosestTrav& T, ClosestStack& K, float bound) {   // next no
     }
     return kNoRef;
 }
-PT_HD void ctrav_init(ClosestTrav& T, const SceneK& S, F3 o32, int ogrp, F3 d32, float bound) {
+// root: S.bvh_root (two-child walk) or S.qroot (4-wide walk)
+PT_HD void ctrav_init(ClosestTrav& T, const SceneK& S, F3 o32, int ogrp, F3 d32, float bound,
+                      int root) {
     T.o32 = o32;
     T.d32 = d32;
     T.inv = rcp_dir(d32);
@@ -623,7 +625,7 @@ PT_HD void ctrav_init(ClosestTrav& T, const SceneK& S, F3 o32, int ogrp, F3 d32,
     T.top = 0;
     T.tref = kNoRef;
     T.tdist = INFINITY;
-    T.ref = node_dist(S, 0, o32, T.inv, bound) < INFINITY ? S.bvh_root : kNoRef;
+    T.ref = node_dist(S, 0, o32, T.inv, bound) < INFINITY ? root : kNoRef;
 }
 // one internal node (T.ref >= 0): nearer child next, the farther stacked
 PT_HD void ctrav_node(ClosestTrav& T, ClosestStack& K, const SceneK& S, const ClosestAcc* ca) {
@@ -662,7 +664,7 @@ PT_HD void bvh_closest(const SceneK& S, F3 o32, int ogrp, F3 d32, ClosestAcc* ca
                        Counters* cnt) {
     ClosestTrav T;
     ClosestStack K;
-    ctrav_init(T, S, o32, ogrp, d32, ca->b1);
+    ctrav_init(T, S, o32, ogrp, d32, ca->b1, S.bvh_root);
     while (!ctrav_step<COUNT>(T, K, S, ca, sp, cnt)) {
     }
 }
@@ -696,7 +698,8 @@ PT_HD int strav_pop(ShadowTrav& T, ShadowStack& K, const SceneK& S, const Shadow
     return kNoRef;
 }
 template <bool COUNT>
-PT_HD void strav_init(ShadowTrav& T, const SceneK& S, F3 o32, int ogrp, const ShadowSet* sh) {
+PT_HD void strav_init(ShadowTrav& T, const SceneK& S, F3 o32, int ogrp, const ShadowSet* sh,
+                      int root) {
     T.o32 = o32;
     T.ogrp = ogrp;
 #pragma unroll
@@ -712,7 +715,7 @@ PT_HD void strav_init(ShadowTrav& T, const SceneK& S, F3 o32, int ogrp, const Sh
     for (int k = 0; k < kLightSamples; ++k)
         if (((open >> k) & 1u) && box_hit(l, h, T.inv[k], sh->hhi[k])) rays |= 1u << k;
     T.rays = rays;
-    T.ref = rays ? S.bvh_root : kNoRef;
+    T.ref = rays ? root : kNoRef;
 }
 // one internal node (T.ref >= 0): the nearer child (by the smallest |t| of
 // its rays) next, the farther stacked with its rays
@@ -770,9 +773,102 @@ PT_HD void bvh_shadow(const SceneK& S, F3 o32, int ogrp, ShadowSet* sh, const Sp
                       Counters* cnt) {
     ShadowTrav T;
     ShadowStack K;
-    strav_init<COUNT>(T, S, o32, ogrp, sh);
+    strav_init<COUNT>(T, S, o32, ogrp, sh, S.bvh_root);
     while (!strav_step<COUNT>(T, K, S, sh, sp, cnt)) {
     }
+}
+
+// ------------------------------------------------ 4-wide walks (QNode) --
+PT_HD float q_step(uint32_t ex, int a) {   // 2^(byte a - 127)
+    const uint32_t b = ((ex >> (8 * a)) & 0xffu) << 23;
+    float f;
+    memcpy(&f, &b, sizeof f);
+    return f;
+}
+PT_HD float q_byte(uint32_t w, int c) { return (float)((w >> (8 * c)) & 0xffu); }
+// child c's decoded box (exact: pt_prepare.h checks it) relative to o, as
+// cbox_dist forms it
+PT_HD void q_box(const QNode& Q, int c, const float st[3], F3 o, F3* l, F3* h) {
+    l->x = fmaf(q_byte(Q.qlo[0], c), st[0], Q.org[0]) - o.x;
+    l->y = fmaf(q_byte(Q.qlo[1], c), st[1], Q.org[1]) - o.y;
+    l->z = fmaf(q_byte(Q.qlo[2], c), st[2], Q.org[2]) - o.z;
+    h->x = fmaf(q_byte(Q.qhi[0], c), st[0], Q.org[0]) - o.x;
+    h->y = fmaf(q_byte(Q.qhi[1], c), st[1], Q.org[1]) - o.y;
+    h->z = fmaf(q_byte(Q.qhi[2], c), st[2], Q.org[2]) - o.z;
+}
+// 4 (distance, ref, rays) triples in ascending distance (sorting network)
+PT_HD void q_sort4(float d[4], int r[4], uint32_t m[4]) {
+    auto cs = [&](int i, int j) {
+        const bool sw = d[j] < d[i];
+        const float td = sw ? d[j] : d[i], ud = sw ? d[i] : d[j];
+        const int tr = sw ? r[j] : r[i], ur = sw ? r[i] : r[j];
+        const uint32_t tm = sw ? m[j] : m[i], um = sw ? m[i] : m[j];
+        d[i] = td; d[j] = ud; r[i] = tr; r[j] = ur; m[i] = tm; m[j] = um;
+    };
+    cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
+}
+// one 4-wide node of the shadow walk (T.ref >= 0 a QNode): nearest child
+// next, the others stacked farthest first
+template <bool COUNT>
+PT_HD void strav_qnode(ShadowTrav& T, ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
+    const QNode Q = S.qnode[T.ref];
+    const float st[3] = {q_step(Q.ex, 0), q_step(Q.ex, 1), q_step(Q.ex, 2)};
+    float d[4];
+    int r[4];
+    uint32_t m[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        F3 l, h;
+        q_box(Q, c, st, T.o32, &l, &h);
+        float dc = INFINITY;
+        uint32_t mc = 0;
+#pragma unroll
+        for (int k = 0; k < kLightSamples; ++k) {
+            if (!((T.rays >> k) & 1u)) continue;
+            const float e = box_dist(l, h, T.inv[k], sh->hhi[k]);
+            mc |= e < INFINITY ? 1u << k : 0u;
+            dc = fminf(dc, e);
+        }
+        r[c] = Q.ref[c];
+        const bool live = r[c] != kNoRef && mc != 0;
+        d[c] = live ? dc : INFINITY;
+        m[c] = live ? mc : 0u;
+    }
+    q_sort4(d, r, m);
+#pragma unroll
+    for (int c = 3; c >= 1; --c) {
+        if (m[c]) {
+            if (T.tc != 0) K.e[T.top++] = T.tc;
+            T.tc = (int)(((uint32_t)r[c] << 3) | m[c]);
+        }
+    }
+    if (m[0]) {
+        T.ref = r[0];
+        T.rays = m[0];
+    } else {
+        T.ref = strav_pop<COUNT>(T, K, S, sh);
+    }
+}
+// one 4-wide node of the closest walk
+PT_HD void ctrav_qnode(ClosestTrav& T, ClosestStack& K, const SceneK& S, const ClosestAcc* ca) {
+    const QNode Q = S.qnode[T.ref];
+    const float st[3] = {q_step(Q.ex, 0), q_step(Q.ex, 1), q_step(Q.ex, 2)};
+    float d[4];
+    int r[4];
+    uint32_t m[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        F3 l, h;
+        q_box(Q, c, st, T.o32, &l, &h);
+        r[c] = Q.ref[c];
+        d[c] = r[c] != kNoRef ? box_dist(l, h, T.inv, ca->b1) : INFINITY;
+        m[c] = 0;
+    }
+    q_sort4(d, r, m);
+#pragma unroll
+    for (int c = 3; c >= 1; --c)
+        if (d[c] < INFINITY) ctrav_push(T, K, r[c], d[c]);
+    T.ref = d[0] < INFINITY ? r[0] : ctrav_pop(T, K, ca->b1);
 }
 
 // Standalone query (primary rays, the batched intersect_objects API).  d need

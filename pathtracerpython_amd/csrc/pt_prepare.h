@@ -21,6 +21,7 @@ struct HostScene {
     std::vector<UnitF> bunit;
     std::vector<BNode> bnode;
     std::vector<CNode> cnode;
+    std::vector<QNode> qnode;
     std::vector<int32_t> tri_grp;
     std::vector<TriD> trid;
     std::vector<TriS> tris;
@@ -34,6 +35,7 @@ struct HostScene {
 constexpr int kBvhMinTris = 64;   // objects this large are traversed through the BVH
 constexpr int kBvhLeaf = 2;       // units per leaf (at most 7: 3 bits of BNode::leaf)
 constexpr int kBvhBins = 16;
+constexpr int kBvhStackHost = 48;   // = kBvhStack (pt_path.h)
 
 // outward rounding to f32
 inline float f32_down(double x) {
@@ -155,15 +157,104 @@ struct BvhBuilder {
     }
 };
 
+// 4-wide quantised form of the two-child tree (QNode): each node takes the
+// two children of a binary node and keeps opening its internal child of
+// largest surface area until it has 4 children.  Returns the subtree's QNode
+// index (or the leaf code); *stack = the most stack entries a nearest-first
+// walk of the subtree can hold (3 per level at most).
+struct QBuilder {
+    HostScene* H;
+    struct Child { int32_t ref; float lo[3], hi[3]; };
+    static double area(const Child& c) {
+        const double e0 = (double)c.hi[0] - c.lo[0], e1 = (double)c.hi[1] - c.lo[1],
+                     e2 = (double)c.hi[2] - c.lo[2];
+        return e0 * e1 + e1 * e2 + e2 * e0;
+    }
+    // one axis: grid origin / step / codes with exact f32 decode
+    static bool quantise(const Child* ch, int n, int a, QNode* Q) {
+        double plo = INFINITY, phi = -INFINITY;
+        for (int c = 0; c < n; ++c) { plo = std::min(plo, (double)ch[c].lo[a]); phi = std::max(phi, (double)ch[c].hi[a]); }
+        int e = (int)floor(log2(std::max(phi - plo, 1e-30) / 255.0)) - 1;
+        for (; e < 127; ++e) {
+            if (e < -126) continue;
+            const double step = ldexp(1.0, e);
+            const double org = floor(plo / step) * step;
+            if ((double)(float)org != org || ceil((phi - org) / step) > 255.0) continue;
+            bool ok = true;
+            uint32_t lo = 0, hi = 0;
+            for (int c = 0; c < n && ok; ++c) {
+                const double ql = floor(((double)ch[c].lo[a] - org) / step);
+                const double qh = ceil(((double)ch[c].hi[a] - org) / step);
+                const float dl = fmaf((float)ql, (float)step, (float)org);   // the kernel's decode
+                const float dh = fmaf((float)qh, (float)step, (float)org);
+                ok = ql >= 0 && qh <= 255 && (double)dl == org + ql * step &&
+                     (double)dh == org + qh * step && dl <= ch[c].lo[a] && dh >= ch[c].hi[a];
+                lo |= (uint32_t)ql << (8 * c);
+                hi |= (uint32_t)qh << (8 * c);
+            }
+            if (!ok) continue;
+            Q->org[a] = (float)org;
+            Q->ex |= (uint32_t)(e + 127) << (8 * a);
+            Q->qlo[a] = lo;
+            Q->qhi[a] = hi;
+            return true;
+        }
+        return false;
+    }
+    bool failed = false;   // some node could not be quantised exactly
+    int32_t build(int32_t ref, int* stack) {
+        *stack = 0;
+        if (ref < 0) return ref;   // a leaf
+        std::vector<Child> ch;
+        auto open = [&](int32_t r) {
+            const CNode& C = H->cnode[r];
+            Child a{C.c0, {C.lo0[0], C.lo0[1], C.lo0[2]}, {C.hi0[0], C.hi0[1], C.hi0[2]}};
+            Child b{C.c1, {C.lo1[0], C.lo1[1], C.lo1[2]}, {C.hi1[0], C.hi1[1], C.hi1[2]}};
+            ch.push_back(a);
+            ch.push_back(b);
+        };
+        open(ref);
+        while (ch.size() < 4) {
+            int best = -1;
+            for (int i = 0; i < (int)ch.size(); ++i)
+                if (ch[i].ref >= 0 && (best < 0 || area(ch[i]) > area(ch[best]))) best = i;
+            if (best < 0) break;
+            const int32_t r = ch[best].ref;
+            ch.erase(ch.begin() + best);
+            open(r);
+        }
+        const int32_t q = (int32_t)H->qnode.size();
+        H->qnode.push_back(QNode{});
+        QNode Q{};
+        for (int c = 0; c < 4; ++c) Q.ref[c] = kNoRef;
+        for (int a = 0; a < 3; ++a)
+            if (!quantise(ch.data(), (int)ch.size(), a, &Q)) failed = true;
+        int deepest = 0;
+        for (int c = 0; c < (int)ch.size() && !failed; ++c) {
+            int sub = 0;
+            const int32_t r = build(ch[c].ref, &sub);
+            Q.ref[c] = r;
+            deepest = std::max(deepest, sub);
+        }
+        *stack = deepest + (int)ch.size() - 1;
+        H->qnode[q] = Q;
+        return q;
+    }
+};
+
 inline void build_bvh(HostScene* H, double X) {
     H->bnode.clear();
     H->cnode.clear();
+    H->qnode.clear();
     SceneK& K = H->k;
     K.n_bnode = 0;
     K.n_bunit = (int32_t)H->bunit.size();
     K.bvh_min_tri = K.n_tri;
     K.bvh_min_obj = K.n_obj;
     K.bvh_depth = 0;
+    K.n_qnode = 0;
+    K.qroot = kNoRef;
+    K.qstack = kBvhStackHost + 1;   // no 4-wide form
     const int n = (int)H->bunit.size();
     if (n == 0) return;
     BvhBuilder B;
@@ -216,6 +307,16 @@ inline void build_bvh(HostScene* H, double X) {
         C.c1 = ref(b);
     }
     K.bvh_root = ref(0);
+    QBuilder QB{H};
+    int qs = 0;
+    const int32_t qr = QB.build(K.bvh_root, &qs);
+    if (!QB.failed) {
+        K.qroot = qr;
+        K.n_qnode = (int32_t)H->qnode.size();
+        K.qstack = qs + 1;
+    } else {
+        H->qnode.clear();
+    }
 }
 
 inline D3 tri_vertex(const pt_scene_desc* d, int t, int v) {
@@ -483,6 +584,7 @@ inline void bind_host(HostScene* H) {
     H->k.unit = H->unit.data();
     H->k.bnode = H->bnode.data();
     H->k.cnode = H->cnode.data();
+    H->k.qnode = H->qnode.data();
     H->k.bunit = H->bunit.data();
     H->k.tri_grp = H->tri_grp.data();
     H->k.trid = H->trid.data();

@@ -86,7 +86,7 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
     HostScene H;
     if (!prepare_scene(d, &H).empty()) return -1;
     bind_host(&H);
-    if (H.k.n_bnode == 0 || H.k.bvh_depth >= kBvhStack) return -3;
+    if (H.k.n_bnode == 0 || H.k.n_qnode == 0 || H.k.qstack > kBvhStack) return -3;
     int32_t first, rows;
     if (!band_layout(p, &first, &rows)) return -2;
     const size_t n = (size_t)rows * p->width;
@@ -135,10 +135,10 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
                 wf_get_shadow(H.k, SQ[i], &o32, &ogrp, &sh);
                 ShadowTrav T;
                 ShadowStack K;
-                strav_init<false>(T, H.k, o32, ogrp, &sh);
+                strav_init<false>(T, H.k, o32, ogrp, &sh, H.k.qroot);
                 ++ws[0];
-                while (T.ref != kNoRef) {   // strav_step, counted
-                    while (T.ref >= 0) { strav_node<false>(T, K, H.k, &sh); ++ws[1]; }
+                while (T.ref != kNoRef) {   // strav_step over the 4-wide nodes, counted
+                    while (T.ref >= 0) { strav_qnode<false>(T, K, H.k, &sh); ++ws[1]; }
                     if (T.ref != kNoRef) {
                         ++ws[2];
                         ws[3] += (~T.ref) & 7;
@@ -155,10 +155,11 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
                 ClosestTrav T;
                 ClosestStack K;
                 const WfClosestQ& q = CQ[i];
-                ctrav_init(T, H.k, F3{q.o[0], q.o[1], q.o[2]}, q.ogrp, F3{q.d[0], q.d[1], q.d[2]}, ca.b1);
+                ctrav_init(T, H.k, F3{q.o[0], q.o[1], q.o[2]}, q.ogrp, F3{q.d[0], q.d[1], q.d[2]}, ca.b1,
+                           H.k.qroot);
                 ++ws[4];
                 while (T.ref != kNoRef) {   // ctrav_step, counted
-                    while (T.ref >= 0) { ctrav_node(T, K, H.k, &ca); ++ws[5]; }
+                    while (T.ref >= 0) { ctrav_qnode(T, K, H.k, &ca); ++ws[5]; }
                     if (T.ref != kNoRef) {
                         ++ws[6];
                         ws[7] += (~T.ref) & 7;
@@ -177,6 +178,17 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
         }
     if (steps_out) *steps_out = busy;
     if (walk_stats) memcpy(walk_stats, ws, sizeof(ws));
+    return 0;
+}
+
+// BVH shape: out = {n_bnode, bvh_depth, n_qnode, qstack}
+int hc_bvh_info(const pt_scene_desc* d, int32_t* out) {
+    HostScene H;
+    if (!prepare_scene(d, &H).empty()) return -1;
+    out[0] = H.k.n_bnode;
+    out[1] = H.k.bvh_depth;
+    out[2] = H.k.n_qnode;
+    out[3] = H.k.qstack;
     return 0;
 }
 
