@@ -236,6 +236,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
 #ifndef PT_WALK_WAVES
 #define PT_WALK_WAVES 1
 #endif
+constexpr int kWalkStack = 32;   // entries of a walk kernel's shared-memory stack
 __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPath* __restrict__ W,
                                                    WfShadowQ* __restrict__ SQ,
                                                    const int32_t* __restrict__ list, int32_t* counters,
@@ -243,10 +244,15 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
     const int32_t count = counters[0];
     int32_t slot = -1;
     bool exhausted = false;
+    // the walk stack in shared memory (this kernel has no other use for it):
+    // kWalkStack x 4 B per lane, 32 KB per block
+    __shared__ int stack[kWalkStack][256];
+    const ShadowStack K{&stack[0][threadIdx.x], 256};
     ShadowSet sh;
     ShadowTrav T;
-    ShadowStack K;
     T.ref = kNoRef;
+    int pl = kNoRef;         // postponed leaf and its rays
+    uint32_t plr = 0;
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
@@ -264,14 +270,27 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
             }
         }
         if (__all(slot < 0)) break;
-        while (true) {   // node phase (wave-uniform loop)
+        // node phase (wave-uniform loop).  Speculative: a lane that reaches a
+        // leaf postpones it (pl) and keeps walking, so a turn can test two
+        // leaves per lane and fewer lanes idle in this loop.
+        while (true) {
+            if (slot >= 0 && T.ref <= -2 && pl == kNoRef) {
+                pl = T.ref;
+                plr = T.rays;
+                T.ref = strav_pop<false>(T, K, S, &sh);
+            }
             const bool desc = slot >= 0 && T.ref >= 0;
             const int32_t nd = (int32_t)__popcll(__ballot(desc));
             // end it early only when some lane has a leaf to test (progress)
-            if (nd == 0 || (nd <= thr && __any(slot >= 0 && T.ref <= -2))) break;
+            if (nd == 0 || (nd <= thr && __any(slot >= 0 && (pl != kNoRef || T.ref <= -2)))) break;
             if (desc) strav_qnode<false>(T, K, S, &sh);
         }
-        if (slot >= 0 && T.ref <= -2) strav_leaf<false>(T, K, S, &sh, Spill{W[slot].sp, 1}, nullptr);
+        if (slot >= 0) {
+            const Spill sp{W[slot].sp, 1};
+            if (pl != kNoRef) strav_units<false>(T, S, &sh, sp, nullptr, pl, plr);
+            pl = kNoRef;
+            if (T.ref <= -2) strav_leaf<false>(T, K, S, &sh, sp, nullptr);
+        }
         if (slot >= 0 && T.ref == kNoRef) {
             int occ = 0;
 #pragma unroll
@@ -294,6 +313,7 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfP
     ClosestTrav T;
     ClosestStack K;
     T.ref = kNoRef;
+    int pl = kNoRef;         // postponed leaf
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
@@ -311,14 +331,22 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfP
             }
         }
         if (__all(slot < 0)) break;
-        while (true) {   // node phase (wave-uniform loop)
+        while (true) {   // node phase, speculative as in k_wf_shadow
+            if (slot >= 0 && T.ref <= -2 && pl == kNoRef) {
+                pl = T.ref;
+                T.ref = ctrav_pop(T, K, ca.b1);
+            }
             const bool desc = slot >= 0 && T.ref >= 0;
             const int32_t nd = (int32_t)__popcll(__ballot(desc));
-            // end it early only when some lane has a leaf to test (progress)
-            if (nd == 0 || (nd <= thr && __any(slot >= 0 && T.ref <= -2))) break;
+            if (nd == 0 || (nd <= thr && __any(slot >= 0 && (pl != kNoRef || T.ref <= -2)))) break;
             if (desc) ctrav_qnode(T, K, S, &ca);
         }
-        if (slot >= 0 && T.ref <= -2) ctrav_leaf<false>(T, K, S, &ca, Spill{W[slot].sp, 1}, nullptr);
+        if (slot >= 0) {
+            const Spill sp{W[slot].sp, 1};
+            if (pl != kNoRef) ctrav_units<false>(T, S, &ca, sp, nullptr, pl);
+            pl = kNoRef;
+            if (T.ref <= -2) ctrav_leaf<false>(T, K, S, &ca, sp, nullptr);
+        }
         if (slot >= 0 && T.ref == kNoRef) {
             CQ[slot].a1 = ca.a1;
             CQ[slot].a2 = ca.a2;
@@ -563,7 +591,7 @@ static uint32_t choose_split(uint32_t npix, int32_t spp) {
 static int32_t wf_thr() {
     static const int32_t v = [] {
         const char* e = getenv("PT_WF_THR");
-        return e ? (int32_t)strtol(e, nullptr, 10) : 4;
+        return e ? (int32_t)strtol(e, nullptr, 10) : 8;
     }();
     return v;
 }
@@ -647,7 +675,7 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     // only the single kernel implements)
     const bool wavefront = s->dev.n_bnode > 0 && !count && !f64 &&
                            !(p->flags & PT_FLAG_MEGAKERNEL) && s->dev.n_qnode > 0 &&
-                           s->dev.qstack <= kBvhStack;
+                           s->dev.qstack <= kWalkStack;
     if (wavefront) {
         rc = render_wavefront(s, R, grid, out_dev, st);
         if (!rc && stats) memset(stats, 0, sizeof(*stats));

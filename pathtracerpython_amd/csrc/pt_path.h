@@ -638,16 +638,22 @@ PT_HD void ctrav_node(ClosestTrav& T, ClosestStack& K, const SceneK& S, const Cl
     if (df < INFINITY) ctrav_push(T, K, rf, df);
     T.ref = dn < INFINITY ? rn : ctrav_pop(T, K, ca->b1);
 }
-// the leaf T.ref (<= -2: leaf codes have a unit count >= 1), then the next entry
+// the units of leaf `ref` (<= -2: leaf codes have a unit count >= 1)
 template <bool COUNT>
-PT_HD void ctrav_leaf(ClosestTrav& T, ClosestStack& K, const SceneK& S, ClosestAcc* ca,
-                      const Spill& sp, Counters* cnt) {
-    const int code = ~T.ref, u0 = code >> 3, nu = code & 7;
+PT_HD void ctrav_units(const ClosestTrav& T, const SceneK& S, ClosestAcc* ca, const Spill& sp,
+                       Counters* cnt, int ref) {
+    const int code = ~ref, u0 = code >> 3, nu = code & 7;
     for (int i = 0; i < nu; ++i) {
         const UnitF U = S.bunit[u0 + i];
         fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, false, true, nullptr,
                                  T.d32, ca, sp, cnt, 8u);
     }
+}
+// the leaf T.ref, then the next entry
+template <bool COUNT>
+PT_HD void ctrav_leaf(ClosestTrav& T, ClosestStack& K, const SceneK& S, ClosestAcc* ca,
+                      const Spill& sp, Counters* cnt) {
+    ctrav_units<COUNT>(T, S, ca, sp, cnt, T.ref);
     T.ref = ctrav_pop(T, K, ca->b1);
 }
 // one "while-while" round: walk internal nodes to the next leaf, test it;
@@ -683,15 +689,19 @@ struct ShadowTrav {
     int top;
     int tc;                   // cached top entry (0: empty; a real entry has a ray bit)
 };
+// a strided view: a per-lane local array (stride 1, scratch memory) or a
+// column of a shared-memory array (stride = block size; the walk kernels)
 struct ShadowStack {
-    int e[kBvhStack];
+    int* e;
+    int stride;
+    PT_HD int& operator[](int i) const { return e[i * stride]; }
 };
 template <bool COUNT>
-PT_HD int strav_pop(ShadowTrav& T, ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
+PT_HD int strav_pop(ShadowTrav& T, const ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
     const uint32_t open = shadow_open<COUNT>(S, sh);
     while (T.tc != 0) {
         const int e = T.tc;
-        T.tc = T.top > 0 ? K.e[--T.top] : 0;
+        T.tc = T.top > 0 ? K[--T.top] : 0;
         T.rays = (uint32_t)e & open & 7u;
         if (T.rays) return e >> 3;
     }
@@ -720,7 +730,7 @@ PT_HD void strav_init(ShadowTrav& T, const SceneK& S, F3 o32, int ogrp, const Sh
 // one internal node (T.ref >= 0): the nearer child (by the smallest |t| of
 // its rays) next, the farther stacked with its rays
 template <bool COUNT>
-PT_HD void strav_node(ShadowTrav& T, ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
+PT_HD void strav_node(ShadowTrav& T, const ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
     const CNode C = S.cnode[T.ref];
     uint32_t m0 = 0, m1 = 0;
     float d0 = INFINITY, d1 = INFINITY;
@@ -738,7 +748,7 @@ PT_HD void strav_node(ShadowTrav& T, ShadowStack& K, const SceneK& S, const Shad
     const uint32_t mn = near0 ? m0 : m1, mf = near0 ? m1 : m0;
     const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
     if (mf) {
-        if (T.tc != 0) K.e[T.top++] = T.tc;
+        if (T.tc != 0) K[T.top++] = T.tc;
         T.tc = (int)(((uint32_t)rf << 3) | mf);
     }
     if (mn) {
@@ -748,21 +758,27 @@ PT_HD void strav_node(ShadowTrav& T, ShadowStack& K, const SceneK& S, const Shad
         T.ref = strav_pop<COUNT>(T, K, S, sh);
     }
 }
-// the leaf T.ref (<= -2) with the rays that reached it, then the next entry
+// the units of leaf `ref` (<= -2) against the rays `rays` that reached it
 template <bool COUNT>
-PT_HD void strav_leaf(ShadowTrav& T, ShadowStack& K, const SceneK& S, ShadowSet* sh,
-                      const Spill& sp, Counters* cnt) {
-    const int code = ~T.ref, u0 = code >> 3, nu = code & 7;
+PT_HD void strav_units(const ShadowTrav& T, const SceneK& S, ShadowSet* sh, const Spill& sp,
+                       Counters* cnt, int ref, uint32_t rays) {
+    const int code = ~ref, u0 = code >> 3, nu = code & 7;
     for (int i = 0; i < nu; ++i) {
         const UnitF U = S.bunit[u0 + i];
         fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, true, false, sh,
-                                 F3{0.f, 0.f, 0.f}, nullptr, sp, cnt, T.rays);
+                                 F3{0.f, 0.f, 0.f}, nullptr, sp, cnt, rays);
     }
+}
+// the leaf T.ref with the rays that reached it, then the next entry
+template <bool COUNT>
+PT_HD void strav_leaf(ShadowTrav& T, const ShadowStack& K, const SceneK& S, ShadowSet* sh,
+                      const Spill& sp, Counters* cnt) {
+    strav_units<COUNT>(T, S, sh, sp, cnt, T.ref, T.rays);
     T.ref = strav_pop<COUNT>(T, K, S, sh);
 }
 // one "while-while" round; returns true when the traversal has ended
 template <bool COUNT>
-PT_HD bool strav_step(ShadowTrav& T, ShadowStack& K, const SceneK& S, ShadowSet* sh,
+PT_HD bool strav_step(ShadowTrav& T, const ShadowStack& K, const SceneK& S, ShadowSet* sh,
                       const Spill& sp, Counters* cnt) {
     while (T.ref >= 0) strav_node<COUNT>(T, K, S, sh);
     if (T.ref != kNoRef) strav_leaf<COUNT>(T, K, S, sh, sp, cnt);
@@ -772,7 +788,8 @@ template <bool COUNT>
 PT_HD void bvh_shadow(const SceneK& S, F3 o32, int ogrp, ShadowSet* sh, const Spill& sp,
                       Counters* cnt) {
     ShadowTrav T;
-    ShadowStack K;
+    int buf[kBvhStack];
+    const ShadowStack K{buf, 1};
     strav_init<COUNT>(T, S, o32, ogrp, sh, S.bvh_root);
     while (!strav_step<COUNT>(T, K, S, sh, sp, cnt)) {
     }
@@ -810,7 +827,7 @@ PT_HD void q_sort4(float d[4], int r[4], uint32_t m[4]) {
 // one 4-wide node of the shadow walk (T.ref >= 0 a QNode): nearest child
 // next, the others stacked farthest first
 template <bool COUNT>
-PT_HD void strav_qnode(ShadowTrav& T, ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
+PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
     const QNode Q = S.qnode[T.ref];
     const float st[3] = {q_step(Q.ex, 0), q_step(Q.ex, 1), q_step(Q.ex, 2)};
     float d[4];
@@ -838,7 +855,7 @@ PT_HD void strav_qnode(ShadowTrav& T, ShadowStack& K, const SceneK& S, const Sha
 #pragma unroll
     for (int c = 3; c >= 1; --c) {
         if (m[c]) {
-            if (T.tc != 0) K.e[T.top++] = T.tc;
+            if (T.tc != 0) K[T.top++] = T.tc;
             T.tc = (int)(((uint32_t)r[c] << 3) | m[c]);
         }
     }

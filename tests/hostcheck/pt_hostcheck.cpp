@@ -134,7 +134,8 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
                 int ogrp;
                 wf_get_shadow(H.k, SQ[i], &o32, &ogrp, &sh);
                 ShadowTrav T;
-                ShadowStack K;
+                int buf[kBvhStack];
+                const ShadowStack K{buf, 1};
                 strav_init<false>(T, H.k, o32, ogrp, &sh, H.k.qroot);
                 ++ws[0];
                 while (T.ref != kNoRef) {   // strav_step over the 4-wide nodes, counted
