@@ -251,8 +251,8 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
     ShadowSet sh;
     ShadowTrav T;
     T.ref = kNoRef;
-    int pl = kNoRef;         // postponed leaf and its rays
-    uint32_t plr = 0;
+    int pl = kNoRef, pl2 = kNoRef;   // postponed leaves and their rays
+    uint32_t plr = 0, plr2 = 0;
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
@@ -274,9 +274,9 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
         // leaf postpones it (pl) and keeps walking, so a turn can test two
         // leaves per lane and fewer lanes idle in this loop.
         while (true) {
-            if (slot >= 0 && T.ref <= -2 && pl == kNoRef) {
-                pl = T.ref;
-                plr = T.rays;
+            if (slot >= 0 && T.ref <= -2 && pl2 == kNoRef) {
+                if (pl == kNoRef) { pl = T.ref; plr = T.rays; }
+                else { pl2 = T.ref; plr2 = T.rays; }
                 T.ref = strav_pop<false>(T, K, S, &sh);
             }
             const bool desc = slot >= 0 && T.ref >= 0;
@@ -288,7 +288,8 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
         if (slot >= 0) {
             const Spill sp{W[slot].sp, 1};
             if (pl != kNoRef) strav_units<false>(T, S, &sh, sp, nullptr, pl, plr);
-            pl = kNoRef;
+            if (pl2 != kNoRef) strav_units<false>(T, S, &sh, sp, nullptr, pl2, plr2);
+            pl = pl2 = kNoRef;
             if (T.ref <= -2) strav_leaf<false>(T, K, S, &sh, sp, nullptr);
         }
         if (slot >= 0 && T.ref == kNoRef) {
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfP
     ClosestTrav T;
     ClosestStack K;
     T.ref = kNoRef;
-    int pl = kNoRef;         // postponed leaf
+    int pl = kNoRef, pl2 = kNoRef;   // postponed leaves
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
@@ -332,8 +333,9 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfP
         }
         if (__all(slot < 0)) break;
         while (true) {   // node phase, speculative as in k_wf_shadow
-            if (slot >= 0 && T.ref <= -2 && pl == kNoRef) {
-                pl = T.ref;
+            if (slot >= 0 && T.ref <= -2 && pl2 == kNoRef) {
+                if (pl == kNoRef) pl = T.ref;
+                else pl2 = T.ref;
                 T.ref = ctrav_pop(T, K, ca.b1);
             }
             const bool desc = slot >= 0 && T.ref >= 0;
@@ -344,7 +346,8 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfP
         if (slot >= 0) {
             const Spill sp{W[slot].sp, 1};
             if (pl != kNoRef) ctrav_units<false>(T, S, &ca, sp, nullptr, pl);
-            pl = kNoRef;
+            if (pl2 != kNoRef) ctrav_units<false>(T, S, &ca, sp, nullptr, pl2);
+            pl = pl2 = kNoRef;
             if (T.ref <= -2) ctrav_leaf<false>(T, K, S, &ca, sp, nullptr);
         }
         if (slot >= 0 && T.ref == kNoRef) {
