@@ -422,6 +422,8 @@ struct pt_scene {
     // and counters, one allocation grown on demand
     void* wf = nullptr;
     size_t wf_slots = 0;
+    hipStream_t wf_side = nullptr;             // the closest walks run beside the shadow walks
+    hipEvent_t wf_ev_shade = nullptr, wf_ev_walk = nullptr;
 };
 
 namespace {
@@ -484,6 +486,9 @@ void pt_scene_destroy(pt_scene* s) {
         if (s->stats) (void)hipFree(s->stats);
         if (s->out_dev) (void)hipFree(s->out_dev);
         if (s->wf) (void)hipFree(s->wf);
+        if (s->wf_ev_shade) (void)hipEventDestroy(s->wf_ev_shade);
+        if (s->wf_ev_walk) (void)hipEventDestroy(s->wf_ev_walk);
+        if (s->wf_side) (void)hipStreamDestroy(s->wf_side);
         if (s->ev0) (void)hipEventDestroy(s->ev0);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
         if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -617,6 +622,11 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
         if (hipMalloc(&s->wf, need) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc wavefront buffers");
         s->wf_slots = slots;
     }
+    if (!s->wf_side) {
+        HIPCHK(hipStreamCreateWithFlags(&s->wf_side, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&s->wf_ev_shade, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&s->wf_ev_walk, hipEventDisableTiming));
+    }
     char* b = (char*)s->wf;
     WfPath* W = (WfPath*)b;
     WfShadowQ* SQ = (WfShadowQ*)(b + off_s);
@@ -634,10 +644,16 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
         hipLaunchKernelGGL(k_wf_shade, grid, dim3(256), 0, st, s->dev, R, step, W, SQ, CQ, lists,
                            counters, (uint32_t)slots);
         if (step + 1 < steps) {
+            // the two walks only read the shade step's output and write
+            // disjoint records: the closest walks run on a side stream
+            HIPCHK(hipEventRecord(s->wf_ev_shade, st));
+            HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
+            hipLaunchKernelGGL(k_wf_closest, dim3(walk_blocks), dim3(256), 0, s->wf_side, s->dev, W,
+                               CQ, (const int32_t*)(lists + slots), counters + 2, wf_thr());
+            HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
             hipLaunchKernelGGL(k_wf_shadow, dim3(walk_blocks), dim3(256), 0, st, s->dev, W, SQ,
                                (const int32_t*)lists, counters, wf_thr());
-            hipLaunchKernelGGL(k_wf_closest, dim3(walk_blocks), dim3(256), 0, st, s->dev, W, CQ,
-                               (const int32_t*)(lists + slots), counters + 2, wf_thr());
+            HIPCHK(hipStreamWaitEvent(st, s->wf_ev_walk, 0));
         }
     }
     hipLaunchKernelGGL(k_wf_final, grid, dim3(256), 0, st, s->dev, R, (const WfPath*)W, out_dev);
