@@ -84,7 +84,9 @@ if "K5" in only:
         linf, sec = check_pixels(r, fb, W, H, 256, 4, pix)
         small = r.render(64, 64, 2, 4, 9, out_f64=True)
         small64 = r.render(64, 64, 2, 4, 9, out_f64=True, force_f64=True)
+        smallmk = r.render(64, 64, 2, 4, 9, out_f64=True, megakernel=True)
         emit("K5", W, H, 256, 4, False, ms, linf, len(pix),
              {"triangles": int(r.packed.n_tri), "ingest_bvh_upload_s": round(setup, 2),
-              "oracle_s": round(sec, 1),
-              "bitwise_eq_forced_f64_64x64x2": bool(np.array_equal(small, small64))})
+              "oracle_s": round(sec, 1), "path": "wavefront (shade + persistent walk kernels)",
+              "bitwise_eq_forced_f64_64x64x2": bool(np.array_equal(small, small64)),
+              "bitwise_eq_single_kernel_64x64x2": bool(np.array_equal(small, smallmk))})
