@@ -10,7 +10,7 @@ determinism) cover the whole image."""
 import numpy as np
 import pytest
 
-from conftest import golden_renders, random_scene
+from conftest import golden_renders, multi_mesh_scene, random_scene
 from oracle import oracle
 from pathtracerpython_amd import _native
 from pathtracerpython_amd.pack import pack_scene
@@ -148,6 +148,21 @@ def test_random_mesh_scene(tmp_path):
     assert np.abs(to_list_order(fb) - ref).max() <= TOL
     with Renderer(sc) as r:   # wavefront (default for BVH scenes) == single kernel
         assert np.array_equal(fb, r.render(48, 48, 4, 5, 8, out_f64=True, megakernel=True))
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_two_meshes_first_in_scene_order(tmp_path, seed):
+    """Two BVH objects ahead of a small object and the walls in scene order
+    (the leaked colour of main.py:70 across BVH objects): wavefront ==
+    single kernel == forced f64, and the oracle to rounding."""
+    sc = multi_mesh_scene(tmp_path, seed)
+    pk = pack_scene(sc)
+    with Renderer(sc) as r:
+        wf = r.render(40, 40, 3, 4, seed, out_f64=True)
+        assert np.array_equal(wf, r.render(40, 40, 3, 4, seed, out_f64=True, megakernel=True))
+        assert np.array_equal(wf, r.render(40, 40, 3, 4, seed, out_f64=True, force_f64=True))
+    ref, _ = oracle.render(pk, 40, 40, 3, 4, seed)
+    assert np.abs(to_list_order(wf) - ref).max() <= TOL
 
 
 @pytest.fixture(scope="module")

@@ -8,7 +8,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from conftest import golden_renders, hc_render, random_scene
+from conftest import golden_renders, hc_render, multi_mesh_scene, random_scene
 from oracle import oracle
 from pathtracerpython_amd._abi import PT_FLAG_RR, make_params
 from pathtracerpython_amd.pack import pack_scene
@@ -219,3 +219,17 @@ def test_wavefront_needs_a_bvh(hostcheck, packed):
     assert hostcheck.hc_render_wavefront(C.byref(packed.desc), C.byref(p),
                                          out.ctypes.data_as(C.POINTER(C.c_double)), None,
                                          None) == -3
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_two_meshes_first_in_scene_order(hostcheck, tmp_path, seed):
+    """Two BVH objects ahead of a small object and the walls in scene order:
+    the single-kernel lane code (hybrid and forced f64) against the oracle
+    with the reference's work counters, and the wavefront form against it."""
+    pk = pack_scene(multi_mesh_scene(tmp_path, seed))
+    info = (C.c_int32 * 4)()
+    assert hostcheck.hc_bvh_info(C.byref(pk.desc), info) == 0
+    assert info[0] > 1 and info[2] > 0   # a BVH and its 4-wide form
+    _bvh_case(hostcheck, pk, 20, 20, 2, 4, seed)
+    _wavefront_case(hostcheck, pk, 20, 20, 2, 4, seed)
+    _wavefront_case(hostcheck, pk, 16, 16, 2, 5, seed + 7, PT_FLAG_RR)
