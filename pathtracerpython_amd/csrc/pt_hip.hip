@@ -408,6 +408,7 @@ __global__ __launch_bounds__(256) void k_color(SceneK S, const int32_t* __restri
 // ---------------------------------------------------------------- API --
 struct pt_scene {
     int device = 0;
+    int n_cu = 256;   // compute units of the device (MI355X: 256 in 8 XCDs)
     HostScene host;
     SceneK dev{};
     float xbound = 0.f;
@@ -507,11 +508,13 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     if (!err.empty()) { delete s; return fail(PT_EINVAL, err); }
     if (hipGetDevice(&s->device) != hipSuccess) { delete s; return fail(PT_EHIP, "hipGetDevice failed"); }
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, s->device) == hipSuccess &&
-        std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
-        std::string arch = prop.gcnArchName;
-        delete s;
-        return fail(PT_ENODEV, "device is " + arch + ", this build targets gfx950 only");
+    if (hipGetDeviceProperties(&prop, s->device) == hipSuccess) {
+        if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+            std::string arch = prop.gcnArchName;
+            delete s;
+            return fail(PT_ENODEV, "device is " + arch + ", this build targets gfx950 only");
+        }
+        if (prop.multiProcessorCount > 0) s->n_cu = prop.multiProcessorCount;
     }
     HostScene& H = s->host;
     constexpr int kArrays = 12;
@@ -633,9 +636,15 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     WfClosestQ* CQ = (WfClosestQ*)(b + off_c);
     int32_t* lists = (int32_t*)(b + off_l);
     int32_t* counters = (int32_t*)(b + off_n);
-    // persistent walk grids: enough work-items to fill the chip, no more
-    // than the queries could use
-    const unsigned walk_blocks = std::min<unsigned>(grid.x, 4096u);
+    // persistent walk grids: 3 blocks per CU (K5 512^2x64: 256 blocks
+    // 271 ms, 512 174, 768 169, 1024 178, 4096 188); PT_WF_WALK_BLOCKS
+    // overrides it for tuning sweeps
+    static const unsigned cap_env = [] {
+        const char* e = getenv("PT_WF_WALK_BLOCKS");
+        return e ? (unsigned)strtoul(e, nullptr, 10) : 0u;
+    }();
+    const unsigned walk_blocks =
+        std::max(1u, std::min<unsigned>(grid.x, cap_env ? cap_env : 3u * (unsigned)s->n_cu));
     const int32_t per_slot = (R.spp + (int32_t)R.split - 1) / (int32_t)R.split;
     const int32_t steps = per_slot * R.bounces + 2;
     HIPCHK(hipEventRecord(s->ev0, st));
