@@ -312,7 +312,10 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfP
     bool exhausted = false;
     ClosestAcc ca = closest_init();
     ClosestTrav T;
-    ClosestStack K;
+    // the walk stack in shared memory: kWalkStack x 6 B per lane
+    __shared__ int sref[kWalkStack][256];
+    __shared__ uint16_t sdist[kWalkStack][256];
+    const ClosestStack K{&sref[0][threadIdx.x], &sdist[0][threadIdx.x], 256};
     T.ref = kNoRef;
     int pl = kNoRef, pl2 = kNoRef;   // postponed leaves
     while (true) {
@@ -637,14 +640,18 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     int32_t* lists = (int32_t*)(b + off_l);
     int32_t* counters = (int32_t*)(b + off_n);
     // persistent walk grids: 3 blocks per CU (K5 512^2x64: 256 blocks
-    // 271 ms, 512 174, 768 169, 1024 178, 4096 188); PT_WF_WALK_BLOCKS
-    // overrides it for tuning sweeps
-    static const unsigned cap_env = [] {
-        const char* e = getenv("PT_WF_WALK_BLOCKS");
+    // 271 ms, 512 174, 768 169, 1024 178, 4096 188); PT_WF_SHADOW_BLOCKS /
+    // PT_WF_CLOSEST_BLOCKS override them for tuning sweeps
+    auto env_blocks = [](const char* name) {
+        const char* e = getenv(name);
         return e ? (unsigned)strtoul(e, nullptr, 10) : 0u;
-    }();
-    const unsigned walk_blocks =
-        std::max(1u, std::min<unsigned>(grid.x, cap_env ? cap_env : 3u * (unsigned)s->n_cu));
+    };
+    static const unsigned env_sh = env_blocks("PT_WF_SHADOW_BLOCKS");
+    static const unsigned env_cl = env_blocks("PT_WF_CLOSEST_BLOCKS");
+    auto blocks = [&](unsigned env) {
+        return std::max(1u, std::min<unsigned>(grid.x, env ? env : 3u * (unsigned)s->n_cu));
+    };
+    const unsigned sh_blocks = blocks(env_sh), cl_blocks = blocks(env_cl);
     const int32_t per_slot = (R.spp + (int32_t)R.split - 1) / (int32_t)R.split;
     const int32_t steps = per_slot * R.bounces + 2;
     HIPCHK(hipEventRecord(s->ev0, st));
@@ -657,10 +664,10 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
             // disjoint records: the closest walks run on a side stream
             HIPCHK(hipEventRecord(s->wf_ev_shade, st));
             HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
-            hipLaunchKernelGGL(k_wf_closest, dim3(walk_blocks), dim3(256), 0, s->wf_side, s->dev, W,
+            hipLaunchKernelGGL(k_wf_closest, dim3(cl_blocks), dim3(256), 0, s->wf_side, s->dev, W,
                                CQ, (const int32_t*)(lists + slots), counters + 2, wf_thr());
             HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
-            hipLaunchKernelGGL(k_wf_shadow, dim3(walk_blocks), dim3(256), 0, st, s->dev, W, SQ,
+            hipLaunchKernelGGL(k_wf_shadow, dim3(sh_blocks), dim3(256), 0, st, s->dev, W, SQ,
                                (const int32_t*)lists, counters, wf_thr());
             HIPCHK(hipStreamWaitEvent(st, s->wf_ev_walk, 0));
         }

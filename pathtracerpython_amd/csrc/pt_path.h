@@ -595,22 +595,60 @@ struct ClosestTrav {
 };
 // The stack arrays live outside the traversal object (a local array indexed
 // at run time is scratch memory; inside the object it would drag the whole
-// object — origin, inverse direction — to scratch with it).
+// object — origin, inverse direction — to scratch with it).  ClosestStack is
+// a strided view: a per-lane local array (ClosestStackLocal, stride 1) or a
+// column of shared-memory arrays (stride = block size; k_wf_closest).
+// Entry distances are kept as the upper 16 bits of the f32 (truncation of a
+// non-negative float rounds down, so the pop check against the shrinking
+// bound is conservative: it may visit a node the exact distance would skip,
+// never the reverse).
 struct ClosestStack {
-    int ref[kBvhStack];
-    float dist[kBvhStack];
+    int* ref;
+    uint16_t* dist;
+    int stride;
 };
-PT_HD void ctrav_push(ClosestTrav& T, ClosestStack& K, int r, float d) {
-    if (T.tref != kNoRef) { K.ref[T.top] = T.tref; K.dist[T.top] = T.tdist; ++T.top; }
+struct ClosestStackLocal {
+    int ref[kBvhStack];
+    uint16_t dist[kBvhStack];
+    PT_HD ClosestStack view() { return ClosestStack{ref, dist, 1}; }
+};
+PT_HD uint16_t dist_down16(float d) {
+    uint32_t b;
+    memcpy(&b, &d, sizeof b);
+    return (uint16_t)(b >> 16);
+}
+PT_HD float dist_up16(uint16_t h) {
+    const uint32_t b = (uint32_t)h << 16;
+    float d;
+    memcpy(&d, &b, sizeof d);
+    return d;
+}
+PT_HD void ctrav_push(ClosestTrav& T, const ClosestStack& K, int r, float d) {
+    if (T.tref != kNoRef) {
+        K.ref[T.top * K.stride] = T.tref;
+#ifndef PT_CSTACK_NODIST
+        K.dist[T.top * K.stride] = dist_down16(T.tdist);
+#endif
+        ++T.top;
+    }
     T.tref = r;
     T.tdist = d;
 }
-PT_HD int ctrav_pop(ClosestTrav& T, ClosestStack& K, float bound) {   // next node within the bound, or kNoRef
+PT_HD int ctrav_pop(ClosestTrav& T, const ClosestStack& K, float bound) {   // next node within the bound, or kNoRef
     while (T.tref != kNoRef) {
         const int r = T.tref;
         const float d = T.tdist;
-        if (T.top > 0) { --T.top; T.tref = K.ref[T.top]; T.tdist = K.dist[T.top]; }
-        else T.tref = kNoRef;
+        if (T.top > 0) {
+            --T.top;
+            T.tref = K.ref[T.top * K.stride];
+#ifndef PT_CSTACK_NODIST
+            T.tdist = dist_up16(K.dist[T.top * K.stride]);
+#else
+            T.tdist = 0.0f;
+#endif
+        } else {
+            T.tref = kNoRef;
+        }
         if (d <= bound) return r;
     }
     return kNoRef;
@@ -628,7 +666,7 @@ PT_HD void ctrav_init(ClosestTrav& T, const SceneK& S, F3 o32, int ogrp, F3 d32,
     T.ref = node_dist(S, 0, o32, T.inv, bound) < INFINITY ? root : kNoRef;
 }
 // one internal node (T.ref >= 0): nearer child next, the farther stacked
-PT_HD void ctrav_node(ClosestTrav& T, ClosestStack& K, const SceneK& S, const ClosestAcc* ca) {
+PT_HD void ctrav_node(ClosestTrav& T, const ClosestStack& K, const SceneK& S, const ClosestAcc* ca) {
     const CNode C = S.cnode[T.ref];
     const float d0 = cbox_dist(C.lo0, C.hi0, T.o32, T.inv, ca->b1);
     const float d1 = cbox_dist(C.lo1, C.hi1, T.o32, T.inv, ca->b1);
@@ -651,7 +689,7 @@ PT_HD void ctrav_units(const ClosestTrav& T, const SceneK& S, ClosestAcc* ca, co
 }
 // the leaf T.ref, then the next entry
 template <bool COUNT>
-PT_HD void ctrav_leaf(ClosestTrav& T, ClosestStack& K, const SceneK& S, ClosestAcc* ca,
+PT_HD void ctrav_leaf(ClosestTrav& T, const ClosestStack& K, const SceneK& S, ClosestAcc* ca,
                       const Spill& sp, Counters* cnt) {
     ctrav_units<COUNT>(T, S, ca, sp, cnt, T.ref);
     T.ref = ctrav_pop(T, K, ca->b1);
@@ -659,7 +697,7 @@ PT_HD void ctrav_leaf(ClosestTrav& T, ClosestStack& K, const SceneK& S, ClosestA
 // one "while-while" round: walk internal nodes to the next leaf, test it;
 // returns true when the traversal has ended
 template <bool COUNT>
-PT_HD bool ctrav_step(ClosestTrav& T, ClosestStack& K, const SceneK& S, ClosestAcc* ca,
+PT_HD bool ctrav_step(ClosestTrav& T, const ClosestStack& K, const SceneK& S, ClosestAcc* ca,
                       const Spill& sp, Counters* cnt) {
     while (T.ref >= 0) ctrav_node(T, K, S, ca);
     if (T.ref != kNoRef) ctrav_leaf<COUNT>(T, K, S, ca, sp, cnt);
@@ -669,7 +707,8 @@ template <bool COUNT>
 PT_HD void bvh_closest(const SceneK& S, F3 o32, int ogrp, F3 d32, ClosestAcc* ca, const Spill& sp,
                        Counters* cnt) {
     ClosestTrav T;
-    ClosestStack K;
+    ClosestStackLocal L;
+    const ClosestStack K = L.view();
     ctrav_init(T, S, o32, ogrp, d32, ca->b1, S.bvh_root);
     while (!ctrav_step<COUNT>(T, K, S, ca, sp, cnt)) {
     }
@@ -867,7 +906,7 @@ PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, con
     }
 }
 // one 4-wide node of the closest walk
-PT_HD void ctrav_qnode(ClosestTrav& T, ClosestStack& K, const SceneK& S, const ClosestAcc* ca) {
+PT_HD void ctrav_qnode(ClosestTrav& T, const ClosestStack& K, const SceneK& S, const ClosestAcc* ca) {
     const QNode Q = S.qnode[T.ref];
     const float st[3] = {q_step(Q.ex, 0), q_step(Q.ex, 1), q_step(Q.ex, 2)};
     float d[4];

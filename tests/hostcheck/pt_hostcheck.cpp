@@ -154,7 +154,8 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
             if (want[i] & kWfWantClosest) {
                 ClosestAcc ca = wf_get_acc(CQ[i]);
                 ClosestTrav T;
-                ClosestStack K;
+                ClosestStackLocal L;
+                const ClosestStack K = L.view();
                 const WfClosestQ& q = CQ[i];
                 ctrav_init(T, H.k, F3{q.o[0], q.o[1], q.o[2]}, q.ogrp, F3{q.d[0], q.d[1], q.d[2]}, ca.b1,
                            H.k.qroot);
