@@ -582,7 +582,15 @@ static int validate(const pt_render_params* p) {
     return PT_OK;
 }
 
-static uint32_t choose_split(uint32_t npix, int32_t spp) {
+// Lanes (wavefront: path slots) per pixel.  Cornell-type scenes: ~2M lanes
+// fill the chip.  BVH scenes render through the wavefront kernels, whose
+// steps drain the whole slot pool between launches: more slots make fewer,
+// longer steps and amortise each step's tail (K5 512^2 x 64 spp: 2M slots
+// 161.6 ms, 4M 147.1, 8M 140.5, 16M 139.3; 1024^2 x 256 spp: 2M 2586 ms,
+// 8M 2170, 16M 2096, 32M 2071).  16M slots hold 6.5 GB of path and query
+// state.  The single kernel uses the same split, so its framebuffer stays
+// bitwise equal to the wavefront one.
+static uint32_t choose_split(uint32_t npix, int32_t spp, bool bvh) {
     static const long env = [] {
         const char* e = getenv("PT_SPLIT");
         return e ? strtol(e, nullptr, 10) : 0L;
@@ -595,7 +603,8 @@ static uint32_t choose_split(uint32_t npix, int32_t spp) {
         return s;
     }
     uint32_t s = 1;
-    const uint64_t target = (uint64_t)1 << 21;   // ~32k waves: ~8 rounds of 4 waves x 4 SIMDs x 256 CUs
+    // ~32k waves: ~8 rounds of 4 waves x 4 SIMDs x 256 CUs
+    const uint64_t target = (uint64_t)1 << (bvh ? 24 : 21);
     while (s < cap && (uint64_t)npix * s * 2 <= target) s *= 2;
     return s;
 }
@@ -698,7 +707,7 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     R.sample_begin = p->sample_begin;
     R.out_f64 = (p->flags & PT_FLAG_OUT_F64) ? 1 : 0;
     R.npix = (uint32_t)rows * (uint32_t)p->width;
-    R.split = choose_split(R.npix, p->spp);
+    R.split = choose_split(R.npix, p->spp, s->dev.n_bnode > 0);
     R.split_log2 = 0;
     while ((1u << R.split_log2) < R.split) ++R.split_log2;
     const uint64_t threads = (uint64_t)R.npix * R.split;
