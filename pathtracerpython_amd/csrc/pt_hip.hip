@@ -611,14 +611,17 @@ static uint32_t choose_split(uint32_t npix, int32_t spp, bool bvh) {
     return s;
 }
 
-// node-phase exit threshold of the walk kernels (lanes still descending);
-// PT_WF_THR overrides it for tuning sweeps
-static int32_t wf_thr() {
-    static const int32_t v = [] {
-        const char* e = getenv("PT_WF_THR");
-        return e ? (int32_t)strtol(e, nullptr, 10) : 8;
-    }();
-    return v;
+// node-phase exit threshold of the walk kernels (lanes still descending).
+// At 16M slots (K5 512^2 x 64 spp): 4 / 8 / 12 / 16 / 20 / 24 / 32 / 48 ->
+// 149 / 140 / 134 / 131 / 129 / 128 / 130 / 174 ms.  PT_WF_THR_SHADOW /
+// PT_WF_THR_CLOSEST override it for tuning sweeps.
+static int32_t wf_thr(bool shadow) {
+    auto env = [](const char* name) {
+        const char* e = getenv(name);
+        return e ? (int32_t)strtol(e, nullptr, 10) : 24;
+    };
+    static const int32_t sh = env("PT_WF_THR_SHADOW"), cl = env("PT_WF_THR_CLOSEST");
+    return shadow ? sh : cl;
 }
 
 // The wavefront render of a BVH scene (pt_wavefront.h): per step one shade
@@ -676,10 +679,10 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
             HIPCHK(hipEventRecord(s->wf_ev_shade, st));
             HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
             hipLaunchKernelGGL(k_wf_closest, dim3(cl_blocks), dim3(256), 0, s->wf_side, s->dev, W,
-                               CQ, (const int32_t*)(lists + slots), counters + 2, wf_thr());
+                               CQ, (const int32_t*)(lists + slots), counters + 2, wf_thr(false));
             HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
             hipLaunchKernelGGL(k_wf_shadow, dim3(sh_blocks), dim3(256), 0, st, s->dev, W, SQ,
-                               (const int32_t*)lists, counters, wf_thr());
+                               (const int32_t*)lists, counters, wf_thr(true));
             HIPCHK(hipStreamWaitEvent(st, s->wf_ev_walk, 0));
         }
     }

@@ -1,5 +1,5 @@
 """Time the K5 wavefront render under different environment settings (dev
-tool).  Usage: k5_env_sweep.py W SPP VAR v1 v2 ...   e.g. PT_WF_THR 0 8 16"""
+tool).  Usage: k5_env_sweep.py W SPP VAR v1 v2 ...   e.g. PT_WF_THR_SHADOW 8 16 24"""
 import os, subprocess, sys, tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
