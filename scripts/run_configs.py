@@ -6,8 +6,9 @@ bench line is bench.py's K2).  Writes one JSON object per line to stdout.
   K2  512x512, 64 spp, 4 bounces    = bench.py's workload; oracle on 4 rows
   K3  1024x1024, 1024 spp, 8 b + RR oracle on 2 rows (all 1024 spp)
   K5  100k-triangle mesh, 1024x1024, 256 spp, 4 b   oracle on 64 pixels
-K4 (4096^2 x 4096 spp over 8 GPUs) is the driver's multi-GPU run of bench.py.
-Usage: run_configs.py [K1,K2,K3,K5]"""
+  K4  4096x4096, 4096 spp, 4 b: one GPU's row band (iy % 8 == 0) of the 8-GPU split;
+      oracle on 32 pixels of the band
+Usage: run_configs.py [K1,K2,K3,K4,K5]"""
 import json, os, sys, tempfile, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -20,12 +21,12 @@ from pathtracerpython_amd.synth import write_k5_scene
 
 scene_reader.VERBOSE = False
 CORNELL = os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl")
-only = sys.argv[1].split(",") if len(sys.argv) > 1 else ["K1", "K2", "K3", "K5"]
+only = sys.argv[1].split(",") if len(sys.argv) > 1 else ["K1", "K2", "K3", "K4", "K5"]
 
 
-def timed(r, W, H, spp, B, rr=False, reps=2):
-    p = r.params(W, H, spp, B, 9, rr=rr, out_f64=True)
-    fb = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+def timed(r, W, H, spp, B, rr=False, reps=2, **band):
+    p = r.params(W, H, spp, B, 9, rr=rr, out_f64=True, **band)
+    fb = torch.zeros((r.band_rows(p), W, 3), dtype=torch.float64, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     ms = []
     for _ in range(reps):
@@ -72,6 +73,27 @@ with Renderer(scene_reader.Scene(CORNELL)) as r:
         pix = [ix * H + iy for iy in rows for ix in range(0, W, 8)]
         linf, sec = check_pixels(r, fb, W, H, 1024, 8, pix, rr=True)
         emit("K3", W, H, 1024, 8, True, ms, linf, len(pix), {"oracle_s": round(sec, 1)})
+    if "K4" in only:
+        # one GPU's share of K4 (4096^2, 4096 spp, 4 bounces over 8 GPUs): the
+        # rows iy % 8 == 0, as rank 0 of bench.py's 8-GPU row interleave
+        W = H = 4096
+        fb, ms = timed(r, W, H, 4096, 4, reps=1, row_step=8, row_phase=0)
+        band = list(range(0, H, 8))
+        rs = np.random.RandomState(1)
+        pick = [(int(ix), band[int(j)]) for ix, j in zip(rs.choice(W, 32), rs.choice(len(band), 32))]
+        t0 = time.time()
+        cols, _ = oracle.render(r.packed, W, H, 4096, 4, 9,
+                                pixels=np.asarray([ix * H + iy for ix, iy in pick], dtype=np.int64),
+                                threads=16)
+        rows = len(band)
+        got = np.array([fb[rows - 1 - band.index(iy), ix] for ix, iy in pick])
+        d = {"config": "K4 (1 of 8 row bands)", "width": W, "height": H, "spp": 4096, "bounces": 4,
+             "rr": False, "rows": rows, "kernel_ms": round(ms, 3),
+             "Mpath_per_s": round(W * rows * 4096 / ms / 1e3, 2),
+             "linf_vs_oracle_f64": float(np.abs(got - cols).max()), "oracle_pixels": len(pick),
+             "oracle_s": round(time.time() - t0, 1),
+             "note": "8 GPUs render one such band each; + one RCCL gather of 4096x512x3 per rank"}
+        print(json.dumps(d), flush=True)
 if "K5" in only:
     sdl = write_k5_scene(tempfile.mkdtemp(), n_tris=100_000, seed=0, size=1024)
     t0 = time.time()
