@@ -55,7 +55,11 @@ def test_matches_reference_goldens(R, packed, name, g):
 # --------------------------------------------------------- vs oracle --
 @pytest.mark.parametrize("W,H,spp,B,seed,rr", [(96, 96, 4, 5, 3, False), (37, 19, 7, 4, 1, False),
                                                (1, 1, 3, 6, 2, False), (64, 64, 5, 8, 4, True),
-                                               (50, 50, 2, 1, 9, False)])
+                                               (50, 50, 2, 1, 9, False),
+                                               # several lanes per pixel (split 8, 32, and 8
+                                               # with a ragged 100 = 4 x 13 + 4 x 12 samples)
+                                               (40, 24, 64, 3, 6, False), (16, 16, 256, 2, 7, True),
+                                               (20, 12, 100, 3, 8, False)])
 def test_matches_oracle(R, packed, W, H, spp, B, seed, rr):
     from pathtracerpython_amd._abi import PT_FLAG_RR
     fb = R.render(W, H, spp, B, seed, rr=rr, out_f64=True)
@@ -115,10 +119,10 @@ def test_deterministic_and_seeded(R):
 def test_interleaved_bands_assemble(R):
     from pathtracerpython_amd.distributed import assemble, max_band_rows
     W, H, world = 160, 130, 4
-    full = R.render(W, H, 4, 4, 7, out_f64=True)
+    full = R.render(W, H, 32, 4, 7, out_f64=True)   # 4 lanes per pixel
     tiles = []
     for r in range(world):
-        t = R.render(W, H, 4, 4, 7, out_f64=True, row_step=world, row_phase=r)
+        t = R.render(W, H, 32, 4, 7, out_f64=True, row_step=world, row_phase=r)
         pad = np.zeros((max_band_rows(H, world), W, 3))
         pad[:t.shape[0]] = t
         tiles.append(pad)
