@@ -46,6 +46,10 @@ struct RenderK {
     uint32_t split, split_log2;
     uint32_t npix;
     int32_t out_f64;
+    // single kernel, launch drain: the pixels from tail_pix on (the image's
+    // top rows, dispatched last) get 2^tail_log2 lanes each, from lane
+    // tail_lane (a multiple of 64) on; tail_pix = npix: none
+    uint32_t tail_pix, tail_lane, tail_log2;
 };
 
 struct StatsDev { unsigned long long v[8]; };
@@ -105,8 +109,9 @@ __device__ __forceinline__ SlotJob slot_job(const SceneK& S, const RenderK& R, u
 
 // Sum of a pixel's sample colours over its `split` work-items (fixed xor
 // order: deterministic), / spp (main.py:277), into the framebuffer.
-__device__ __forceinline__ void store_pixel(const RenderK& R, const SlotJob& j, D3 acc, void* out) {
-    for (uint32_t m = 1; m < R.split; m <<= 1) {
+__device__ __forceinline__ void store_pixel(const RenderK& R, const SlotJob& j, D3 acc, void* out,
+                                            uint32_t split) {
+    for (uint32_t m = 1; m < split; m <<= 1) {
         acc.x += __shfl_xor(acc.x, (int)m);
         acc.y += __shfl_xor(acc.y, (int)m);
         acc.z += __shfl_xor(acc.z, (int)m);
@@ -135,9 +140,12 @@ __global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __
     // (slot_job's mapping written out: the register allocation of this kernel
     // is sensitive to what stays live across the render loop)
     const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t pl = tid >> R.split_log2;
-    const uint32_t c = tid & (R.split - 1u);
-    const bool valid = pl < R.npix;
+    const bool tail = tid >= R.tail_lane;   // wave-uniform
+    const uint32_t slog = tail ? R.tail_log2 : R.split_log2, split = 1u << slog;
+    const uint32_t lt = tail ? tid - R.tail_lane : tid;
+    const uint32_t pl = (tail ? R.tail_pix : 0u) + (lt >> slog);
+    const uint32_t c = lt & (split - 1u);
+    const bool valid = pl < (tail ? R.npix : R.tail_pix);
     Counters cnt = {};
     D3 acc = d3(0, 0, 0);
     int32_t row_local = 0, ix = 0;
@@ -149,12 +157,12 @@ __global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __
         const double x = linspace_at(S.ortho[0], S.ortho[2], R.W, ix);
         const double y = linspace_at(S.ortho[1], S.ortho[3], R.H, iy);
         const D3 d0 = d3(x - eye.x, y - eye.y, 0.0 - eye.z);
-        const int32_t ns = ((int32_t)c < R.spp) ? (R.spp - (int32_t)c + (int32_t)R.split - 1) / (int32_t)R.split : 0;
+        const int32_t ns = ((int32_t)c < R.spp) ? (R.spp - (int32_t)c + (int32_t)split - 1) / (int32_t)split : 0;
         LaneJob J;
         J.seed = R.seed;
         J.pixel = (uint32_t)ix * (uint32_t)R.H + (uint32_t)iy;
         J.sample0 = R.sample_begin + (int32_t)c;
-        J.sample_stride = (int32_t)R.split;
+        J.sample_stride = (int32_t)split;
         J.n_samples = ns;
         J.bounces = R.bounces;
         J.rr_depth = R.rr_depth;
@@ -168,7 +176,7 @@ __global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __
     j.c = c;
     j.row_local = row_local;
     j.ix = ix;
-    store_pixel(R, j, acc, out);
+    store_pixel(R, j, acc, out, split);
     flush_counters<COUNT>(cnt, st);
 }
 
@@ -368,7 +376,7 @@ __global__ __launch_bounds__(256) void k_wf_final(SceneK S, RenderK R, const WfP
     const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
     const SlotJob j = slot_job(S, R, tid);
     const D3 acc = j.valid ? ld3(W[tid].acc) : d3(0, 0, 0);
-    store_pixel(R, j, acc, out);
+    store_pixel(R, j, acc, out, R.split);
 }
 
 __global__ __launch_bounds__(256) void k_intersect(SceneK S, const double* __restrict__ rays,
@@ -715,7 +723,33 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     R.split = choose_split(R.npix, p->spp, s->dev.n_bnode > 0);
     R.split_log2 = 0;
     while ((1u << R.split_log2) < R.split) ++R.split_log2;
-    const uint64_t threads = (uint64_t)R.npix * R.split;
+    R.tail_pix = R.npix;
+    R.tail_lane = R.npix * R.split;
+    R.tail_log2 = R.split_log2;
+    if (s->dev.n_bnode == 0) {
+        // The launch drains for about one wave lifetime (~1 ms at K2: 7% of
+        // its wave-slots idle).  The image's top sixteenth of
+        // rows (iy >= H - ceil(H/16), dispatched last, also in every
+        // interleaved band) gets 8x the lanes per pixel, so the last dispatch
+        // round is short waves.  K2 6.70 -> 6.49 ms; sixteenth / eighth /
+        // quarter of the rows at 2x / 4x / 8x lanes all land within 6.49-6.54.
+        // A pixel's lanes depend only on (iy, H, spp) and the band's base
+        // split, so band renders still assemble bit for bit.
+        constexpr int kTailFrac = 16;
+        constexpr uint32_t kTailMul = 3;   // log2 of the lane multiplier
+        uint32_t cap = 64;
+        while (cap > 1 && (int32_t)cap > p->spp) cap >>= 1;
+        const uint32_t tl = std::min(R.split_log2 + kTailMul, (uint32_t)__builtin_ctz(cap));
+        const int32_t thresh = p->height - (p->height + kTailFrac - 1) / kTailFrac;
+        int32_t ra = 0;   // band rows below the threshold (a prefix: rows ascend)
+        while (ra < rows && first + ra * p->row_step < thresh) ++ra;
+        if (tl > R.split_log2 && ra < rows) {
+            R.tail_pix = (uint32_t)ra * (uint32_t)p->width;
+            R.tail_lane = (R.tail_pix * R.split + 63u) & ~63u;
+            R.tail_log2 = tl;
+        }
+    }
+    const uint64_t threads = (uint64_t)R.tail_lane + ((uint64_t)(R.npix - R.tail_pix) << R.tail_log2);
     const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
     const bool count = (p->flags & PT_FLAG_COUNT) != 0;
     const bool f64 = (p->flags & PT_FLAG_FORCE_F64) != 0;
