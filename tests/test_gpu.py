@@ -129,6 +129,26 @@ def test_interleaved_bands_assemble(R):
     assert np.array_equal(assemble(tiles, H), full)
 
 
+def test_tail_rows_ragged(R, packed):
+    """The single kernel's last rows run at 8x lanes per pixel (launch drain,
+    DESIGN.md §4): a ragged size where the tail's first lane needs padding to
+    a wave boundary (21 x 37 pixels x 8 lanes = 6216), every pixel vs the
+    oracle, and interleaved bands (own tails) assembling bit for bit."""
+    from pathtracerpython_amd.distributed import assemble, max_band_rows
+    W, H, spp, B, seed = 37, 23, 64, 3, 11
+    fb = R.render(W, H, spp, B, seed, out_f64=True)
+    ref, _ = oracle.render(packed, W, H, spp, B, seed)
+    assert np.abs(to_list_order(fb) - ref).max() <= TOL
+    world = 3
+    tiles = []
+    for r in range(world):
+        t = R.render(W, H, spp, B, seed, out_f64=True, row_step=world, row_phase=r)
+        pad = np.zeros((max_band_rows(H, world), W, 3))
+        pad[:t.shape[0]] = t
+        tiles.append(pad)
+    assert np.array_equal(assemble(tiles, H), fb)
+
+
 def test_contiguous_band(R):
     full = R.render(64, 64, 2, 4, 3)
     band = R.render(64, 64, 2, 4, 3, row_begin=10, row_end=30)
