@@ -1,7 +1,7 @@
 """Per-wave start/end clocks of one K2 launch (dev tool; needs a library built
 with the wave-time instrumentation, passed as PT_HIP_LIB with PT_DEV_OLD_LIB=1).
 Prints the occupancy profile: how long the launch runs below full occupancy
-at its start and end."""
+at its start and end.  Usage: wave_times.py [W] [spp] [waves in the launch]."""
 import ctypes as C, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -19,7 +19,7 @@ for _ in range(3):
     r.render_device(p, out.data_ptr(), s)
 torch.cuda.synchronize()
 lib = _native.lib()
-nw = min(W * W * 8 // 64, 1 << 20)
+nw = min(int(sys.argv[3]) if len(sys.argv) > 3 else W * W * 8 // 64, 1 << 20)
 buf = np.zeros(2 * nw, dtype=np.uint64)
 assert lib.pt_dev_wave_times(buf.ctypes.data_as(C.c_void_p), C.c_size_t(2 * nw)) == 0
 st, en = buf[0::2].astype(np.int64), buf[1::2].astype(np.int64)
