@@ -74,6 +74,30 @@ struct alignas(16) UnitF {   // 128 B: two s_load_dwordx16
 };
 static_assert(sizeof(UnitF) == 128, "UnitF is two scalar x16 loads");
 
+// The BVH's single-triangle units in 64 B (two per cache line: the walks'
+// leaf working set halves).  eo and eh are bfloat16 rounded up, the direction
+// bounds (eq, qhi) the maxima over the BVH's units (SceneK::bvh_eq ...), ed is
+// derived from g (ed <= g * kEdPerG, see pt_prepare.h), the object comes from
+// tri_obj.  Wider bounds only widen the undecided band, which is decided in
+// f64, so verdicts stay exact.
+struct alignas(16) UnitC {
+    float n[3], cn;
+    TriB tri;
+    int32_t t, grp;
+    float g;
+    uint32_t eoeh;   // bf16 of eo (low half) and of eh (high half), rounded up
+};
+PT_HD float bf16_lo(uint32_t w) { const uint32_t b = w << 16; float f; memcpy(&f, &b, 4); return f; }
+PT_HD float bf16_hi(uint32_t w) { const uint32_t b = w & 0xffff0000u; float f; memcpy(&f, &b, 4); return f; }
+// bf16 of a finite x >= 0, rounded up
+inline uint32_t bf16_up(float x) {
+    uint32_t b;
+    __builtin_memcpy(&b, &x, 4);
+    return (b >> 16) + ((b & 0xffffu) ? 1u : 0u);
+}
+static_assert(sizeof(UnitC) == 64, "UnitC is 64 B");
+constexpr float kEdPerG = 1.25f * 0x1p-21f;   // s * 8u (pt_prepare.h: ed = 2 s 8u M, g >= 2 M (1 + 1e-3))
+
 // f64 exact record: the reference's plane normal and edges (utils.py:109-111,
 // :78-80).  cvp = dot(vp, v1).
 struct alignas(16) TriD {
@@ -170,6 +194,10 @@ struct SceneK {
     const QNode* qnode;          // [n_qnode] the 4-wide quantised form (wavefront walks)
     int32_t n_qnode, qroot;      // qroot: a QNode, or ~code for a leaf root
     int32_t qstack, pad4;        // stack entries a 4-wide walk can need
+    const UnitC* bunitc;         // [n_bunit] bunit in 64-B form, or null (some unit is a
+                                 // coplanar pair or degenerate: the walks read bunit)
+    float bvh_eh, bvh_eq, bvh_qhi;   // maxima over bunit
+    int32_t bvh_obj1;            // the BVH's one object, or -1 (several: from tri_obj)
 };
 
 // ------------------------------------------------------------------ RNG --

@@ -245,6 +245,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
 #define PT_WALK_WAVES 1
 #endif
 constexpr int kWalkStack = 32;   // entries of a walk kernel's shared-memory stack
+template <bool UC>
 __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPath* __restrict__ W,
                                                    WfShadowQ* __restrict__ SQ,
                                                    const int32_t* __restrict__ list, int32_t* counters,
@@ -295,10 +296,10 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
         }
         if (slot >= 0) {
             const Spill sp{W[slot].sp, 1};
-            if (pl != kNoRef) strav_units<false>(T, S, &sh, sp, nullptr, pl, plr);
-            if (pl2 != kNoRef) strav_units<false>(T, S, &sh, sp, nullptr, pl2, plr2);
+            if (pl != kNoRef) strav_units<false, UC>(T, S, &sh, sp, nullptr, pl, plr);
+            if (pl2 != kNoRef) strav_units<false, UC>(T, S, &sh, sp, nullptr, pl2, plr2);
             pl = pl2 = kNoRef;
-            if (T.ref <= -2) strav_leaf<false>(T, K, S, &sh, sp, nullptr);
+            if (T.ref <= -2) strav_leaf<false, UC>(T, K, S, &sh, sp, nullptr);
         }
         if (slot >= 0 && T.ref == kNoRef) {
             int occ = 0;
@@ -311,6 +312,7 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
     }
 }
 
+template <bool UC>
 __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
                                                     WfClosestQ* __restrict__ CQ,
                                                     const int32_t* __restrict__ list, int32_t* counters,
@@ -356,10 +358,10 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfP
         }
         if (slot >= 0) {
             const Spill sp{W[slot].sp, 1};
-            if (pl != kNoRef) ctrav_units<false>(T, S, &ca, sp, nullptr, pl);
-            if (pl2 != kNoRef) ctrav_units<false>(T, S, &ca, sp, nullptr, pl2);
+            if (pl != kNoRef) ctrav_units<false, UC>(T, S, &ca, sp, nullptr, pl);
+            if (pl2 != kNoRef) ctrav_units<false, UC>(T, S, &ca, sp, nullptr, pl2);
             pl = pl2 = kNoRef;
-            if (T.ref <= -2) ctrav_leaf<false>(T, K, S, &ca, sp, nullptr);
+            if (T.ref <= -2) ctrav_leaf<false, UC>(T, K, S, &ca, sp, nullptr);
         }
         if (slot >= 0 && T.ref == kNoRef) {
             CQ[slot].a1 = ca.a1;
@@ -528,18 +530,19 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         if (prop.multiProcessorCount > 0) s->n_cu = prop.multiProcessorCount;
     }
     HostScene& H = s->host;
-    constexpr int kArrays = 12;
+    constexpr int kArrays = 13;
     const size_t sz[kArrays] = {H.unit.size() * sizeof(UnitF), H.trid.size() * sizeof(TriD),
                                 H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
                                 H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
                                 H.light_cum.size() * sizeof(double),
                                 H.tri_grp.size() * sizeof(int32_t),
                                 H.bnode.size() * sizeof(BNode), H.bunit.size() * sizeof(UnitF),
-                                H.cnode.size() * sizeof(CNode), H.qnode.size() * sizeof(QNode)};
+                                H.cnode.size() * sizeof(CNode), H.qnode.size() * sizeof(QNode),
+                                H.bunitc.size() * sizeof(UnitC)};
     const void* src[kArrays] = {H.unit.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
                                 H.mat.data(), H.light_tri.data(), H.light_cum.data(),
                                 H.tri_grp.data(), H.bnode.data(), H.bunit.data(), H.cnode.data(),
-                                H.qnode.data()};
+                                H.qnode.data(), H.bunitc.data()};
     size_t off[kArrays], total = 0;
     for (int i = 0; i < kArrays; ++i) { off[i] = total; total += align_up(sz[i]); }
     int rc = PT_OK;
@@ -566,6 +569,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     s->dev.bunit = (const UnitF*)(b + off[9]);
     s->dev.cnode = (const CNode*)(b + off[10]);
     s->dev.qnode = (const QNode*)(b + off[11]);
+    s->dev.bunitc = H.bunitc.empty() ? nullptr : (const UnitC*)(b + off[12]);
     s->xbound = box_bound(H);
     *out = s;
     return rc;
@@ -686,11 +690,19 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
             // disjoint records: the closest walks run on a side stream
             HIPCHK(hipEventRecord(s->wf_ev_shade, st));
             HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
-            hipLaunchKernelGGL(k_wf_closest, dim3(cl_blocks), dim3(256), 0, s->wf_side, s->dev, W,
-                               CQ, (const int32_t*)(lists + slots), counters + 2, wf_thr(false));
+            if (s->dev.bunitc)
+                hipLaunchKernelGGL(k_wf_closest<true>, dim3(cl_blocks), dim3(256), 0, s->wf_side, s->dev,
+                                   W, CQ, (const int32_t*)(lists + slots), counters + 2, wf_thr(false));
+            else
+                hipLaunchKernelGGL(k_wf_closest<false>, dim3(cl_blocks), dim3(256), 0, s->wf_side, s->dev,
+                                   W, CQ, (const int32_t*)(lists + slots), counters + 2, wf_thr(false));
             HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
-            hipLaunchKernelGGL(k_wf_shadow, dim3(sh_blocks), dim3(256), 0, st, s->dev, W, SQ,
-                               (const int32_t*)lists, counters, wf_thr(true));
+            if (s->dev.bunitc)
+                hipLaunchKernelGGL(k_wf_shadow<true>, dim3(sh_blocks), dim3(256), 0, st, s->dev, W, SQ,
+                                   (const int32_t*)lists, counters, wf_thr(true));
+            else
+                hipLaunchKernelGGL(k_wf_shadow<false>, dim3(sh_blocks), dim3(256), 0, st, s->dev, W, SQ,
+                                   (const int32_t*)lists, counters, wf_thr(true));
             HIPCHK(hipStreamWaitEvent(st, s->wf_ev_walk, 0));
         }
     }

@@ -677,21 +677,45 @@ PT_HD void ctrav_node(ClosestTrav& T, const ClosestStack& K, const SceneK& S, co
     T.ref = dn < INFINITY ? rn : ctrav_pop(T, K, ca->b1);
 }
 // the units of leaf `ref` (<= -2: leaf codes have a unit count >= 1)
-template <bool COUNT>
+// BVH unit i as the walks test it: UC = from the 64-B form (the caller
+// checked S.bunitc; a compile-time choice, so only one record is loaded)
+template <bool UC>
+PT_HD UnitF bvh_unit(const SceneK& S, int i) {
+    if (!UC) return S.bunit[i];
+    const UnitC C = S.bunitc[i];
+    UnitF U;
+    U.n[0] = C.n[0]; U.n[1] = C.n[1]; U.n[2] = C.n[2];
+    U.cn = C.cn;
+    U.eh = bf16_hi(C.eoeh);
+    U.eq = S.bvh_eq;
+    U.qhi = S.bvh_qhi;
+    U.eo = bf16_lo(C.eoeh);
+    U.ed = C.g * kEdPerG;
+    U.g = C.g;
+    U.grp = C.grp;
+    U.count = 1;
+    U.obj = S.bvh_obj1 >= 0 ? S.bvh_obj1 : S.tri_obj[C.t];
+    U.t[0] = U.t[1] = C.t;
+    U.pad = 0;
+    U.tri[0] = C.tri;
+    U.tri[1] = TriB{};
+    return U;
+}
+template <bool COUNT, bool UC = false>
 PT_HD void ctrav_units(const ClosestTrav& T, const SceneK& S, ClosestAcc* ca, const Spill& sp,
                        Counters* cnt, int ref) {
     const int code = ~ref, u0 = code >> 3, nu = code & 7;
     for (int i = 0; i < nu; ++i) {
-        const UnitF U = S.bunit[u0 + i];
+        const UnitF U = bvh_unit<UC>(S, u0 + i);
         fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, false, true, nullptr,
                                  T.d32, ca, sp, cnt, 8u);
     }
 }
 // the leaf T.ref, then the next entry
-template <bool COUNT>
+template <bool COUNT, bool UC = false>
 PT_HD void ctrav_leaf(ClosestTrav& T, const ClosestStack& K, const SceneK& S, ClosestAcc* ca,
                       const Spill& sp, Counters* cnt) {
-    ctrav_units<COUNT>(T, S, ca, sp, cnt, T.ref);
+    ctrav_units<COUNT, UC>(T, S, ca, sp, cnt, T.ref);
     T.ref = ctrav_pop(T, K, ca->b1);
 }
 // one "while-while" round: walk internal nodes to the next leaf, test it;
@@ -798,21 +822,21 @@ PT_HD void strav_node(ShadowTrav& T, const ShadowStack& K, const SceneK& S, cons
     }
 }
 // the units of leaf `ref` (<= -2) against the rays `rays` that reached it
-template <bool COUNT>
+template <bool COUNT, bool UC = false>
 PT_HD void strav_units(const ShadowTrav& T, const SceneK& S, ShadowSet* sh, const Spill& sp,
                        Counters* cnt, int ref, uint32_t rays) {
     const int code = ~ref, u0 = code >> 3, nu = code & 7;
     for (int i = 0; i < nu; ++i) {
-        const UnitF U = S.bunit[u0 + i];
+        const UnitF U = bvh_unit<UC>(S, u0 + i);
         fused_unit<false, COUNT>(S, U, origin_u(U, T.o32), U.grp == T.ogrp, true, false, sh,
                                  F3{0.f, 0.f, 0.f}, nullptr, sp, cnt, rays);
     }
 }
 // the leaf T.ref with the rays that reached it, then the next entry
-template <bool COUNT>
+template <bool COUNT, bool UC = false>
 PT_HD void strav_leaf(ShadowTrav& T, const ShadowStack& K, const SceneK& S, ShadowSet* sh,
                       const Spill& sp, Counters* cnt) {
-    strav_units<COUNT>(T, S, sh, sp, cnt, T.ref, T.rays);
+    strav_units<COUNT, UC>(T, S, sh, sp, cnt, T.ref, T.rays);
     T.ref = strav_pop<COUNT>(T, K, S, sh);
 }
 // one "while-while" round; returns true when the traversal has ended

@@ -19,6 +19,7 @@ namespace pt {
 struct HostScene {
     std::vector<UnitF> unit;
     std::vector<UnitF> bunit;
+    std::vector<UnitC> bunitc;   // bunit in 64-B form (empty: not representable)
     std::vector<BNode> bnode;
     std::vector<CNode> cnode;
     std::vector<QNode> qnode;
@@ -343,6 +344,44 @@ inline float f32_up(double x) {   // round to f32, never below x (x >= 0)
     return f;
 }
 
+// The 64-B form of the BVH units (UnitC, pt_core.h), when every unit is a
+// single non-degenerate triangle: eo and eh rounded up to bfloat16, eq / qhi
+// the maxima over the units (each unit's own bound is <= what the kernel
+// uses: conservative), ed derived from g in the kernel, the object read from
+// tri_obj.
+inline void build_unitc(HostScene* H) {
+    SceneK& K = H->k;
+    H->bunitc.clear();
+    K.bvh_eh = K.bvh_eq = K.bvh_qhi = 0.f;
+    K.bvh_obj1 = -1;
+    if (H->bunit.empty()) return;
+    int obj1 = H->bunit[0].obj;
+    for (const UnitF& U : H->bunit) {
+        if (U.count != 1 || !(U.eh >= 0.f) || !(U.eh < 1e30f) || !(U.eo > 0.f) || !(U.eo < 1e30f) ||
+            !(U.qhi < INFINITY))
+            return;
+        K.bvh_eh = std::max(K.bvh_eh, U.eh);
+        K.bvh_eq = std::max(K.bvh_eq, U.eq);
+        K.bvh_qhi = std::max(K.bvh_qhi, U.qhi);
+        if (U.obj != obj1) obj1 = -1;
+        // ed must not exceed what the kernel derives from g
+        if (!(U.ed <= U.g * kEdPerG)) return;
+    }
+    K.bvh_obj1 = obj1;
+    H->bunitc.resize(H->bunit.size());
+    for (size_t i = 0; i < H->bunit.size(); ++i) {
+        const UnitF& U = H->bunit[i];
+        UnitC& C = H->bunitc[i];
+        for (int a = 0; a < 3; ++a) C.n[a] = U.n[a];
+        C.cn = U.cn;
+        C.tri = U.tri[0];
+        C.t = U.t[0];
+        C.grp = U.grp;
+        C.g = U.g;
+        C.eoeh = bf16_up(U.eo) | bf16_up(U.eh) << 16;
+    }
+}
+
 // Returns "" on success, else an error message.
 inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     if (!d) return "null scene descriptor";
@@ -576,6 +615,7 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     // (~code << 3 | ray mask) in 32 bits
     if (H->bunit.size() >= (size_t(1) << 24)) return "mesh too large: at most 2^24 BVH units";
     build_bvh(H, X);   // needs K.center and K.n_tri
+    build_unitc(H);
     return "";
 }
 
@@ -586,6 +626,7 @@ inline void bind_host(HostScene* H) {
     H->k.cnode = H->cnode.data();
     H->k.qnode = H->qnode.data();
     H->k.bunit = H->bunit.data();
+    H->k.bunitc = H->bunitc.empty() ? nullptr : H->bunitc.data();
     H->k.tri_grp = H->tri_grp.data();
     H->k.trid = H->trid.data();
     H->k.tris = H->tris.data();

@@ -143,7 +143,8 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
                     if (T.ref != kNoRef) {
                         ++ws[2];
                         ws[3] += (~T.ref) & 7;
-                        strav_leaf<false>(T, K, H.k, &sh, sp, nullptr);
+                        if (H.k.bunitc) strav_leaf<false, true>(T, K, H.k, &sh, sp, nullptr);   // as k_wf_shadow
+                        else strav_leaf<false>(T, K, H.k, &sh, sp, nullptr);
                     }
                 }
                 int occ = 0;
@@ -165,7 +166,8 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
                     if (T.ref != kNoRef) {
                         ++ws[6];
                         ws[7] += (~T.ref) & 7;
-                        ctrav_leaf<false>(T, K, H.k, &ca, sp, nullptr);
+                        if (H.k.bunitc) ctrav_leaf<false, true>(T, K, H.k, &ca, sp, nullptr);   // as k_wf_closest
+                        else ctrav_leaf<false>(T, K, H.k, &ca, sp, nullptr);
                     }
                 }
                 CQ[i].a1 = ca.a1; CQ[i].a2 = ca.a2; CQ[i].b1 = ca.b1; CQ[i].i1 = ca.i1;
@@ -191,6 +193,8 @@ int hc_bvh_info(const pt_scene_desc* d, int32_t* out) {
     out[1] = H.k.bvh_depth;
     out[2] = H.k.n_qnode;
     out[3] = H.k.qstack;
+    out[4] = (int32_t)H.bunitc.size();   // the walks' 64-B unit form (0: not used)
+    out[5] = H.k.bvh_obj1;
     return 0;
 }
 

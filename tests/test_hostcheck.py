@@ -227,9 +227,12 @@ def test_two_meshes_first_in_scene_order(hostcheck, tmp_path, seed):
     the single-kernel lane code (hybrid and forced f64) against the oracle
     with the reference's work counters, and the wavefront form against it."""
     pk = pack_scene(multi_mesh_scene(tmp_path, seed))
-    info = (C.c_int32 * 4)()
+    info = (C.c_int32 * 6)()
     assert hostcheck.hc_bvh_info(C.byref(pk.desc), info) == 0
     assert info[0] > 1 and info[2] > 0   # a BVH and its 4-wide form
+    # the walks read the 64-B unit form, objects from tri_obj (two meshes)
+    assert info[4] > 0
+    assert info[5] == -1
     _bvh_case(hostcheck, pk, 20, 20, 2, 4, seed)
     _wavefront_case(hostcheck, pk, 20, 20, 2, 4, seed)
     _wavefront_case(hostcheck, pk, 16, 16, 2, 5, seed + 7, PT_FLAG_RR)
