@@ -613,12 +613,13 @@ static uint32_t choose_split(uint32_t npix, int32_t spp, bool bvh) {
         while (s * 2 <= (uint32_t)env && s * 2 <= cap) s *= 2;
         return s;
     }
-    // up to 16M lanes; the single kernel also keeps >= 8 samples per lane
-    // (fewer leave waves with idle lanes at the end of their regeneration
-    // loop: K2 512^2 x 64 spp at 16M lanes, 1 sample each, 7.11 vs 6.76 ms;
-    // K3 1024^2 x 1024 spp at 2M / 4M / 16M lanes 555 / 539 / 532 ms)
+    // up to 16M slots (BVH) / 32M lanes; the single kernel also keeps >= 8
+    // samples per lane (fewer leave waves with idle lanes at the end of their
+    // regeneration loop: K2 512^2 x 64 spp at 16M lanes, 1 sample each, 7.11
+    // vs 6.76 ms; K3 1024^2 x 1024 spp at 2M / 4M / 16M / 32M lanes 555 / 539
+    // / 527 / 520 ms)
     uint32_t s = 1;
-    const uint64_t target = (uint64_t)1 << 24;
+    const uint64_t target = (uint64_t)1 << (bvh ? 24 : 25);
     while (s < cap && (uint64_t)npix * s * 2 <= target && (bvh || spp / (int32_t)(s * 2) >= 8)) s *= 2;
     return s;
 }
