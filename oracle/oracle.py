@@ -53,6 +53,17 @@ def _d(a):
     return a.ctypes.data_as(_dp)
 
 
+def host_threads():
+    """Host threads this process may use: the CPUs it is pinned to, capped by
+    OMP_NUM_THREADS when set (the GPU box sets it to the CPU share of one
+    GPU; os.cpu_count() there shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, min(n, 256))
+
+
 def render(packed, width, height, spp, bounces, seed, flags=0, rr_depth=3,
            pixels=None, threads=None, sample_begin=0):
     """Averaged colours (n, 3) f64 for reference list indices `pixels`
@@ -66,7 +77,7 @@ def render(packed, width, height, spp, bounces, seed, flags=0, rr_depth=3,
     p = make_params(width, height, spp, bounces, seed, flags, rr_depth,
                     sample_begin=sample_begin)
     st = PtStats()
-    nt = threads or min(64, os.cpu_count() or 1)
+    nt = threads or host_threads()
     rc = lib.oracle_render(C.byref(packed.desc), C.byref(p),
                            pixels.ctypes.data_as(C.POINTER(C.c_int64)),
                            len(pixels), nt, _d(out), C.byref(st))

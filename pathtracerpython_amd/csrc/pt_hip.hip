@@ -585,7 +585,8 @@ int pt_band_rows(const pt_render_params* p, int32_t* rows) {
 static int validate(const pt_render_params* p) {
     if (!p) return fail(PT_EINVAL, "null params");
     if (p->width <= 0 || p->height <= 0) return fail(PT_EINVAL, "width/height must be > 0");
-    if ((int64_t)p->width * p->height > (int64_t)1 << 32) return fail(PT_EINVAL, "image too large for 32-bit pixel keys");
+    // pixel keys k = ix*H + iy and the launch's pixel counts are 32-bit
+    if ((int64_t)p->width * p->height >= (int64_t)1 << 32) return fail(PT_EINVAL, "image too large for 32-bit pixel keys");
     if (p->spp <= 0) return fail(PT_EINVAL, "spp must be > 0");
     if (p->bounces < 0) return fail(PT_EINVAL, "bounces must be >= 0");
     if (p->sample_begin < 0) return fail(PT_EINVAL, "sample_begin must be >= 0");
@@ -594,48 +595,52 @@ static int validate(const pt_render_params* p) {
     return PT_OK;
 }
 
-// Lanes (wavefront: path slots) per pixel.  BVH scenes render through the wavefront kernels, whose
-// steps drain the whole slot pool between launches: more slots make fewer,
-// longer steps and amortise each step's tail (K5 512^2 x 64 spp: 2M slots
-// 161.6 ms, 4M 147.1, 8M 140.5, 16M 139.3; 1024^2 x 256 spp: 2M 2586 ms,
-// 8M 2170, 16M 2096, 32M 2071).  16M slots hold 6.5 GB of path and query
-// state.  The single kernel uses the same split, so its framebuffer stays
-// bitwise equal to the wavefront one.
-static uint32_t choose_split(uint32_t npix, int32_t spp, bool bvh) {
-    static const long env = [] {
-        const char* e = getenv("PT_SPLIT");
-        return e ? strtol(e, nullptr, 10) : 0L;
-    }();
+// Lanes (wavefront: path slots) per pixel: a power of two <= min(64, spp),
+// a function of the FULL image (width x height) and spp only — never of the
+// band a launch renders — so every band of an interleaved multi-GPU split
+// runs each pixel on the same lanes, sums its samples in the same order and
+// the bands assemble to the 1-GPU frame bit for bit.
+//
+// Single kernel: >= 8 samples per lane, at most 2^30 lanes over the full
+// image (K2 512^2 x 64 spp: 8 lanes per pixel; K3 and K4: 64).
+// Wavefront (BVH scenes): path slots hold ~400 B of state each, so at most
+// 16M slots over the full image (K5 512^2 x 64 spp: 2M slots 161.6 ms, 4M
+// 147.1, 8M 140.5, 16M 139.3; 1024^2 x 256 spp: 2M 2586 ms, 16M 2096); an
+// N-way band gets 1/N of them.  The single kernel uses the same split on BVH
+// scenes, so its framebuffer stays bitwise equal to the wavefront one.
+//
+// PT_SPLIT_FIXED (compile-time, tuning builds only) pins the split.
+static uint32_t choose_split(uint64_t image_pixels, int32_t spp, bool bvh) {
     uint32_t cap = 64;
     while (cap > 1 && (int32_t)cap > spp) cap >>= 1;
-    if (env > 0) {
-        uint32_t s = 1;
-        while (s * 2 <= (uint32_t)env && s * 2 <= cap) s *= 2;
-        return s;
-    }
-    // up to 16M slots (BVH) / 32M lanes; the single kernel also keeps >= 8
-    // samples per lane (fewer leave waves with idle lanes at the end of their
-    // regeneration loop: K2 512^2 x 64 spp at 16M lanes, 1 sample each, 7.11
-    // vs 6.76 ms; K3 1024^2 x 1024 spp at 2M / 4M / 16M / 32M lanes 555 / 539
-    // / 527 / 520 ms)
+#ifdef PT_SPLIT_FIXED
+    uint32_t f = 1;
+    while (f * 2 <= (uint32_t)PT_SPLIT_FIXED && f * 2 <= cap) f *= 2;
+    (void)image_pixels; (void)bvh;
+    return f;
+#else
     uint32_t s = 1;
-    const uint64_t target = (uint64_t)1 << (bvh ? 24 : 25);
-    while (s < cap && (uint64_t)npix * s * 2 <= target && (bvh || spp / (int32_t)(s * 2) >= 8)) s *= 2;
+    const uint64_t target = (uint64_t)1 << (bvh ? 24 : 30);
+    while (s < cap && image_pixels * s * 2 <= target && (bvh || spp / (int32_t)(s * 2) >= 8)) s *= 2;
     return s;
+#endif
 }
 
-// node-phase exit threshold of the walk kernels (lanes still descending).
-// At 16M slots (K5 512^2 x 64 spp): 4 / 8 / 12 / 16 / 20 / 24 / 32 / 48 ->
-// 149 / 140 / 134 / 131 / 129 / 128 / 130 / 174 ms.  PT_WF_THR_SHADOW /
-// PT_WF_THR_CLOSEST override it for tuning sweeps.
-static int32_t wf_thr(bool shadow) {
-    auto env = [](const char* name) {
-        const char* e = getenv(name);
-        return e ? (int32_t)strtol(e, nullptr, 10) : 24;
-    };
-    static const int32_t sh = env("PT_WF_THR_SHADOW"), cl = env("PT_WF_THR_CLOSEST");
-    return shadow ? sh : cl;
-}
+// Walk kernels: node-phase exit threshold (lanes still descending) and
+// persistent grid size.  At 16M slots (K5 512^2 x 64 spp) the threshold
+// 4 / 8 / 12 / 16 / 20 / 24 / 32 / 48 -> 149 / 140 / 134 / 131 / 129 / 128 /
+// 130 / 174 ms; grids of 1 / 2 / 3 / 4 / 16 blocks per CU -> 271 / 174 / 169
+// / 178 / 188 ms.  Compile-time (-D) so tuning builds can sweep them; the
+// shipped library has no run-time knobs.
+#ifndef PT_WF_THR_SHADOW
+#define PT_WF_THR_SHADOW 24
+#endif
+#ifndef PT_WF_THR_CLOSEST
+#define PT_WF_THR_CLOSEST 24
+#endif
+#ifndef PT_WF_BLOCKS_PER_CU
+#define PT_WF_BLOCKS_PER_CU 3
+#endif
 
 // The wavefront render of a BVH scene (pt_wavefront.h): per step one shade
 // launch over the path slots, then the two persistent walk launches over the
@@ -666,19 +671,8 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     WfClosestQ* CQ = (WfClosestQ*)(b + off_c);
     int32_t* lists = (int32_t*)(b + off_l);
     int32_t* counters = (int32_t*)(b + off_n);
-    // persistent walk grids: 3 blocks per CU (K5 512^2x64: 256 blocks
-    // 271 ms, 512 174, 768 169, 1024 178, 4096 188); PT_WF_SHADOW_BLOCKS /
-    // PT_WF_CLOSEST_BLOCKS override them for tuning sweeps
-    auto env_blocks = [](const char* name) {
-        const char* e = getenv(name);
-        return e ? (unsigned)strtoul(e, nullptr, 10) : 0u;
-    };
-    static const unsigned env_sh = env_blocks("PT_WF_SHADOW_BLOCKS");
-    static const unsigned env_cl = env_blocks("PT_WF_CLOSEST_BLOCKS");
-    auto blocks = [&](unsigned env) {
-        return std::max(1u, std::min<unsigned>(grid.x, env ? env : 3u * (unsigned)s->n_cu));
-    };
-    const unsigned sh_blocks = blocks(env_sh), cl_blocks = blocks(env_cl);
+    const unsigned wf_blocks =
+        std::max(1u, std::min<unsigned>(grid.x, (unsigned)PT_WF_BLOCKS_PER_CU * (unsigned)s->n_cu));
     const int32_t per_slot = (R.spp + (int32_t)R.split - 1) / (int32_t)R.split;
     const int32_t steps = per_slot * R.bounces + 2;
     HIPCHK(hipEventRecord(s->ev0, st));
@@ -692,18 +686,18 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
             HIPCHK(hipEventRecord(s->wf_ev_shade, st));
             HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
             if (s->dev.bunitc)
-                hipLaunchKernelGGL(k_wf_closest<true>, dim3(cl_blocks), dim3(256), 0, s->wf_side, s->dev,
-                                   W, CQ, (const int32_t*)(lists + slots), counters + 2, wf_thr(false));
+                hipLaunchKernelGGL(k_wf_closest<true>, dim3(wf_blocks), dim3(256), 0, s->wf_side, s->dev,
+                                   W, CQ, (const int32_t*)(lists + slots), counters + 2, PT_WF_THR_CLOSEST);
             else
-                hipLaunchKernelGGL(k_wf_closest<false>, dim3(cl_blocks), dim3(256), 0, s->wf_side, s->dev,
-                                   W, CQ, (const int32_t*)(lists + slots), counters + 2, wf_thr(false));
+                hipLaunchKernelGGL(k_wf_closest<false>, dim3(wf_blocks), dim3(256), 0, s->wf_side, s->dev,
+                                   W, CQ, (const int32_t*)(lists + slots), counters + 2, PT_WF_THR_CLOSEST);
             HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
             if (s->dev.bunitc)
-                hipLaunchKernelGGL(k_wf_shadow<true>, dim3(sh_blocks), dim3(256), 0, st, s->dev, W, SQ,
-                                   (const int32_t*)lists, counters, wf_thr(true));
+                hipLaunchKernelGGL(k_wf_shadow<true>, dim3(wf_blocks), dim3(256), 0, st, s->dev, W, SQ,
+                                   (const int32_t*)lists, counters, PT_WF_THR_SHADOW);
             else
-                hipLaunchKernelGGL(k_wf_shadow<false>, dim3(sh_blocks), dim3(256), 0, st, s->dev, W, SQ,
-                                   (const int32_t*)lists, counters, wf_thr(true));
+                hipLaunchKernelGGL(k_wf_shadow<false>, dim3(wf_blocks), dim3(256), 0, st, s->dev, W, SQ,
+                                   (const int32_t*)lists, counters, PT_WF_THR_SHADOW);
             HIPCHK(hipStreamWaitEvent(st, s->wf_ev_walk, 0));
         }
     }
@@ -733,7 +727,7 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     R.sample_begin = p->sample_begin;
     R.out_f64 = (p->flags & PT_FLAG_OUT_F64) ? 1 : 0;
     R.npix = (uint32_t)rows * (uint32_t)p->width;
-    R.split = choose_split(R.npix, p->spp, s->dev.n_bnode > 0);
+    R.split = choose_split((uint64_t)p->width * (uint64_t)p->height, p->spp, s->dev.n_bnode > 0);
     R.split_log2 = 0;
     while ((1u << R.split_log2) < R.split) ++R.split_log2;
     R.tail_pix = R.npix;
@@ -746,8 +740,8 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
         // interleaved band) gets 8x the lanes per pixel, so the last dispatch
         // round is short waves.  K2 6.70 -> 6.49 ms; sixteenth / eighth /
         // quarter of the rows at 2x / 4x / 8x lanes all land within 6.49-6.54.
-        // A pixel's lanes depend only on (iy, H, spp) and the band's base
-        // split, so band renders still assemble bit for bit.
+        // A pixel's lanes depend only on (iy, W, H, spp), so band renders
+        // still assemble bit for bit.
         constexpr int kTailFrac = 16;
         constexpr uint32_t kTailMul = 3;   // log2 of the lane multiplier
         uint32_t cap = 64;
@@ -756,13 +750,23 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
         const int32_t thresh = p->height - (p->height + kTailFrac - 1) / kTailFrac;
         int32_t ra = 0;   // band rows below the threshold (a prefix: rows ascend)
         while (ra < rows && first + ra * p->row_step < thresh) ++ra;
-        if (tl > R.split_log2 && ra < rows) {
+        // (no tail when the full image's lanes would overflow the 32-bit
+        // lane index: decided on the full image so bands still agree)
+        const uint64_t full_lanes = (uint64_t)thresh * p->width * R.split + 64 +
+                                    (((uint64_t)(p->height - thresh) * (uint64_t)p->width) << tl);
+        if (tl > R.split_log2 && ra < rows && full_lanes < ((uint64_t)1 << 32)) {
             R.tail_pix = (uint32_t)ra * (uint32_t)p->width;
             R.tail_lane = (R.tail_pix * R.split + 63u) & ~63u;
             R.tail_log2 = tl;
         }
     }
     const uint64_t threads = (uint64_t)R.tail_lane + ((uint64_t)(R.npix - R.tail_pix) << R.tail_log2);
+    if ((uint64_t)R.npix * R.split >= ((uint64_t)1 << 32) || threads >= ((uint64_t)1 << 32))
+        return fail(PT_EINVAL, "launch needs 2^32 or more work-items (32-bit lane index)");
+    // launches on one handle share its scratch (wavefront state, counters,
+    // events): order this one after the previous launch, whatever stream
+    // that one ran on
+    if (s->timed) HIPCHK(hipStreamWaitEvent(st, s->ev1, 0));
     const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
     const bool count = (p->flags & PT_FLAG_COUNT) != 0;
     const bool f64 = (p->flags & PT_FLAG_FORCE_F64) != 0;
