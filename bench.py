@@ -1,92 +1,167 @@
 #!/usr/bin/env python3
 """Benchmark: Mega path-samples/sec on the Cornell box (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): objs/cornellroom.sdl, 512x512 pixels,
-64 spp, 4 bounces per GPU.  One step = one render of that image (the whole
-main.py:186-280 loop) with the scene already resident in HBM; the framebuffer
-stays in HBM.  With N GPUs (one process per GPU, torch.distributed over RCCL)
-the job is a 512 x (512*N) image: rank r renders the rows iy % N == r (512 rows,
-a fixed per-GPU share -> weak scaling) and one RCCL gather collects the row
-tiles on rank 0 inside the timed step.
+One step = one render of a fixed frame (the whole main.py:186-280 loop:
+every pixel, every sample, every bounce, the /spp average) with the scene
+resident in HBM, plus — inside the timed step — the RCCL gather of the row
+bands to rank 0 (N > 1), their device-side de-interleave and the framebuffer's
+copy to pinned host memory (kernel + D2H).
+
+Workloads (--config, BASELINE.json configs):
+  k2 (default)  Cornell 512x512, 64 spp, 4 bounces (configs[1], the config the
+                metric is quoted on).
+  k4            Cornell 4096x4096, --spp (default 64; BASELINE's 4096 takes
+                ~3.2 s per step on 8 GPUs), 4 bounces: the K4 frame shape.
+  k5            100k-triangle synthetic mesh 1024x1024, 256 spp, 4 bounces
+                (the BVH / wavefront path).
+Scaling (--scaling): strong (default) — the frame is fixed and N GPUs split
+its rows interleaved (rank r renders iy % N == r), so the 1/2/4/8 curve is
+tile-parallel scaling of one frame; weak (k2 only) — a 512 x (512 N) frame,
+512 rows per GPU.
+
+Multi-GPU: one process per GPU over torch.distributed (backend nccl = RCCL).
+Launched by torch.distributed.run (RANK / WORLD_SIZE in the environment), or,
+for `python bench.py --gpus N`, by this script itself: the parent spawns N
+fresh rank processes (it never touches the GPU) and exits with their status.
 
 Printed on rank 0: one JSON line with the driver's fields plus
-  roofline     : dominant kernel (k_render) achieved FP32 rate from the
-                 reference-semantics ray-triangle test count (exact, from a
-                 counting launch) x 47 FLOP/test over the
-                 HIP-event kernel time, against the 157.3 TF FP32 peak; traffic
-                 from the committed rocprofv3 PMC pass (profiles/)
-  cpu_baseline : the C oracle (a restatement of the reference loop, test
-                 infrastructure) timed on this host on a row sample
+  roofline     : the dominant kernel's achieved rate against its roof.
+                 k2/k4: k_render, FP32 VALU: reference-semantics ray-triangle
+                 tests (exact, from a counting launch) x 47 FLOP (SURVEY.md
+                 §8d) / HIP-event kernel time, vs 157.3 TF/s.  k5: the shadow
+                 walk kernel, HBM: algorithmic bytes (node + leaf records +
+                 query records, from a counting launch) / its HIP-event time,
+                 vs 8 TB/s.  traffic: rocprofv3 PMC bytes per launch from
+                 profiles/, only when measured on the current kernel sources.
+  cpu_baseline : the C oracle (f64 restatement of the reference loop, test
+                 infrastructure) on this host's CPU share, on a bounded sample
   linf_vs_cpu_ref : per-pixel L-inf of this run's framebuffer vs the oracle
-                 on sample rows
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-W = 512
-H_PER_GPU = 512
-SPP = 64
-BOUNCES = 4
 SEED = 9
 FLOP_PER_TEST = 47          # Moller-Trumbore with line semantics
-FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
+FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector (VALU) peak
 HBM_PEAK_GBS = 8000.0
+METRIC = "Mega path-samples/sec on Cornell box; per-pixel L-inf vs CPU ref"
+
+CONFIGS = {
+    "k2": dict(W=512, H=512, spp=64, bounces=4, steps=200, warmup=5,
+               workload="Cornell box (objs/cornellroom.sdl) 512x512 64 spp 4 bounces"),
+    "k4": dict(W=4096, H=4096, spp=64, bounces=4, steps=10, warmup=1,
+               workload="Cornell box 4096x4096 (K4 frame shape) {spp} spp 4 bounces"),
+    "k5": dict(W=1024, H=1024, spp=256, bounces=4, steps=3, warmup=1,
+               workload="Synthetic 100k-triangle random mesh in the Cornell box 1024x1024 "
+                        "256 spp 4 bounces (BVH, wavefront kernels)"),
+}
+# k5 walk kernels' algorithmic bytes: a 4-wide node record
+# (QNode) per node visit, a leaf-unit record (UnitC) per leaf-unit test, the
+# query record read (WfShadowQ) and its 8-B result written per query
+QNODE_B, UNITC_B, SHADOWQ_B, SHADOW_RES_B = 64, 64, 96, 8
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="k2")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
+    ap.add_argument("--spp", type=int, default=None, help="override spp (k4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-check", action="store_true", help="skip L-inf vs the CPU oracle")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c = CONFIGS[a.config]
+    a.steps = c["steps"] if a.steps is None else a.steps
+    a.warmup = c["warmup"] if a.warmup is None else a.warmup
+    if a.scaling == "weak" and a.config != "k2":
+        ap.error("--scaling weak is defined for k2 only")
+    return a
 
 
-def load_traffic():
-    p = os.path.join(ROOT, "profiles", "traffic_k2.json")
+def source_sha():
+    """Hash of the kernel sources (traffic measurements are tied to it)."""
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "pathtracerpython_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".h", ".hip")):
+            h.update(open(os.path.join(csrc, f), "rb").read())
+    h.update(open(os.path.join(ROOT, "include", "pt_capi.h"), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def load_traffic(config):
+    p = os.path.join(ROOT, "profiles", f"traffic_{config}.json")
     if not os.path.exists(p):
         return None, None
     with open(p) as f:
         d = json.load(f)
+    if d.get("source_sha") != source_sha():
+        return None, f"stale: {p} was measured on kernel sources {d.get('source_sha')}"
     return d.get("hbm_bytes_per_launch"), d.get("source")
 
 
 def main():
     args = parse()
+    from pathtracerpython_amd.launch import rank_env, spawn_ranks, under_launcher
+    if args.gpus > 1 and not under_launcher():
+        sys.exit(spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, local, world = rank_env()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    from oracle.oracle import host_threads
     from pathtracerpython_amd import scene_reader
-    from pathtracerpython_amd.distributed import assemble, gather_tiles
+    from pathtracerpython_amd.distributed import band_rows_of, deinterleave
     from pathtracerpython_amd.render import Renderer
     scene_reader.VERBOSE = False
-    scene = scene_reader.Scene(os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl"))
-    H = H_PER_GPU * world
+    cfg = dict(CONFIGS[args.config])
+    if args.spp:
+        cfg["spp"] = args.spp
+    W, H, SPP, B = cfg["W"], cfg["H"], cfg["spp"], cfg["bounces"]
+    if args.scaling == "weak":
+        H = cfg["H"] * world
+    if args.config == "k5":
+        from pathtracerpython_amd.synth import write_k5_scene
+        tmp = tempfile.mkdtemp(prefix="k5_")
+        sdl = write_k5_scene(tmp, n_tris=100_000, seed=0, size=W) if rank == 0 else None
+        if world > 1:   # one writer, every rank reads the same files
+            obj = [sdl]
+            dist.broadcast_object_list(obj, src=0)
+            sdl = obj[0]
+        scene = scene_reader.Scene(sdl)
+    else:
+        scene = scene_reader.Scene(os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl"))
     r = Renderer(scene)
-    p = r.params(W, H, SPP, BOUNCES, SEED, row_begin=0, row_end=H, row_step=world,
-                 row_phase=rank)
+    p = r.params(W, H, SPP, B, SEED, row_begin=0, row_end=H, row_step=world, row_phase=rank)
     rows = r.band_rows(p)
-    assert rows == H_PER_GPU
+    max_rows = (H + world - 1) // world
+    assert rows == len(band_rows_of(H, rank, world))
     stream = torch.cuda.current_stream()
-    tile = torch.zeros((rows, W, 3), dtype=torch.float32, device="cuda")
+    tile = torch.zeros((max_rows, W, 3), dtype=torch.float32, device="cuda")
+    even = H % world == 0
+    if rank == 0:
+        gathered = torch.empty((world, max_rows, W, 3), dtype=torch.float32, device="cuda")
+        frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        host = torch.empty((H, W, 3), dtype=torch.float32).pin_memory()
+        if not even:
+            host_g = torch.empty((world, max_rows, W, 3), dtype=torch.float32).pin_memory()
 
     def step(ev=None):
         if ev:
@@ -95,8 +170,15 @@ def main():
         if ev:
             ev[1].record(stream)
         if world > 1:
-            return gather_tiles(tile)
-        return [tile]
+            dist.gather(tile, gather_list=list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+        if rank == 0:
+            if world == 1:
+                host.copy_(tile[:H], non_blocking=True)
+            elif even:
+                host.copy_(deinterleave(gathered, frame), non_blocking=True)
+            else:   # ragged bands: the gathered tiles go down, assembled after the timed region
+                host_g.copy_(gathered, non_blocking=True)
+        return None
 
     for _ in range(args.warmup):
         step()
@@ -109,7 +191,7 @@ def main():
            for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        out = step(evs[i])
+        step(evs[i])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -118,76 +200,56 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    render_ms = [a.elapsed_time(b) for a, b in evs]
     ms_per_step = elapsed / args.steps * 1e3
     paths = W * H * SPP
     value = paths / (elapsed / args.steps) / 1e6
 
     result = None
     if rank == 0:
-        # exact reference-semantics work of one launch (separate counting launch)
-        pc = r.params(W, H, SPP, BOUNCES, SEED, count=True, row_begin=0, row_end=H,
-                      row_step=world, row_phase=rank)
-        _, st = r.render_params(pc, stats=True)
-        tests = st["closest_tests"] + st["shadow_tests"]
-        k_ms = float(np.mean(kernel_ms))
-        achieved = tests * FLOP_PER_TEST / (k_ms * 1e-3) / 1e12
-        traffic, tsrc = load_traffic()
-        roofline = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                    "traffic": traffic,
-                    "kernel": "k_render<false,false,false>",
-                    "compute_pipe": "VALU f32 (no MFMA: scalar intersection; the MI355X f32 "
-                                    "vector peak equals the f32 MFMA dense peak)",
-                    "work_per_launch": {"ray_triangle_tests": tests,
-                                        "tests_per_path_sample": round(tests / (W * H_PER_GPU * SPP), 2),
-                                        "flop_per_test": FLOP_PER_TEST,
-                                        "f64_fallback_tests": st["f64_fallbacks"],
-                                        "f64_rescans": st["f64_rescans"]},
-                    "kernel_ms_mean": round(k_ms, 4),
-                    "hbm_frac": (round(traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
-                                 if traffic else None),
-                    "traffic_source": tsrc}
-        # correctness of this run: per-pixel L-inf vs the CPU oracle on sample rows
-        linf = None
-        fb = None
-        if not args.no_check or not args.no_cpu_baseline:
-            from oracle import oracle
-            tiles = [t.cpu().numpy() for t in out]
-            fb = assemble(tiles, H) if world > 1 else tiles[0]
+        from oracle import oracle
+        k_ms = float(np.mean(render_ms))
+        if args.config == "k5":
+            roofline = k5_roofline(r, p, k_ms)
+        else:
+            roofline = k_render_roofline(r, p, k_ms, W, rows, SPP, args.config)
+        if world == 1 or even:
+            fb = host.numpy()
+        else:
+            from pathtracerpython_amd.distributed import assemble
+            fb = assemble([t.numpy() for t in host_g.unbind(0)], H)
+        linf, checked = None, None
         if not args.no_check:
-            from oracle import oracle
-            chk_rows = [0, 129, 255, H - 1]
-            pix = np.array([ix * H + iy for iy in chk_rows for ix in range(W)], dtype=np.int64)
-            ref, _ = oracle.render(r.packed, W, H, SPP, BOUNCES, SEED, pixels=pix,
-                                   threads=args.cpu_threads)
-            got = np.stack([fb[H - 1 - iy] for iy in chk_rows]).reshape(-1, 3).astype(np.float64)
+            if args.config == "k5":
+                rs = np.random.RandomState(0)
+                chk = [(int(ix), int(iy)) for ix, iy in zip(rs.choice(W, 4), rs.choice(H, 4))]
+            else:
+                chk = [(ix, iy) for iy in (0, H // 4 + 1, H // 2, H - 1)
+                       for ix in range(0, W, max(1, W // 128))]
+            pix = np.array([ix * H + iy for ix, iy in chk], dtype=np.int64)
+            ref, _ = oracle.render(r.packed, W, H, SPP, B, SEED, pixels=pix, threads=host_threads())
+            got = np.array([fb[H - 1 - iy, ix] for ix, iy in chk], dtype=np.float64)
             linf = float(np.abs(got - ref).max())
+            checked = f"{len(chk)} pixels on rows 0, H/4+1, H/2, H-1" if args.config != "k5" \
+                else f"{len(chk)} random pixels"
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            from oracle import oracle
-            sample_rows = list(range(0, H))
-            pix = np.array([ix * H + iy for iy in sample_rows for ix in range(W)], dtype=np.int64)
-            threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-            t1 = time.perf_counter()
-            oracle.render(r.packed, W, H, SPP, BOUNCES, SEED, pixels=pix, threads=threads)
-            cdt = time.perf_counter() - t1
-            cpu = {"value": round(len(pix) * SPP / cdt / 1e6, 4), "unit": "Mpath-samples/s",
-                   "cores": threads, "kind": "port",
-                   "sample": f"oracle/pt_oracle.c (f64 C restatement of main.py:186-280) on "
-                             f"the whole 512x512 64spp 4-bounce job "
-                             f"({len(pix) * SPP} path samples, {cdt:.1f} s, {threads} threads)"}
+            cpu = cpu_baseline(oracle, r.packed, W, H, SPP, B, args.config)
+        parallel = f"rows interleaved over {world} GPU" + ("s + RCCL gather" if world > 1 else "")
+        wl = cfg["workload"].format(spp=SPP)
+        if args.scaling == "weak":
+            wl = f"Cornell box 512 x (512 N) 64 spp 4 bounces, 512 rows per GPU (weak scaling)"
         result = {
-            "metric": "Mega path-samples/sec on Cornell box; per-pixel L-inf vs CPU ref",
+            "metric": METRIC,
             "value": round(value, 2), "unit": "Mpath-samples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": "f32+f64", "data": "synthetic",
-            "config": {"workload": "Cornell box (objs/cornellroom.sdl) 512x512 64 spp 4 bounces "
-                                   "per GPU; N GPUs render 512x(512N) rows-interleaved + RCCL gather",
-                       "width": W, "height": H, "spp": SPP, "bounces": BOUNCES, "seed": SEED,
-                       "parallelism": f"rows/{world}" + (" + rccl gather" if world > 1 else "")},
-            "linf_vs_cpu_ref": linf,
+            "config": {"workload": wl, "width": W, "height": H, "spp": SPP, "bounces": B,
+                       "seed": SEED, "parallelism": parallel,
+                       "timed_step": "render + (RCCL gather + device de-interleave) + "
+                                     "framebuffer D2H to pinned host memory"},
+            "linf_vs_cpu_ref": linf, "linf_checked": checked,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
@@ -197,6 +259,99 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return result
+
+
+def k_render_roofline(r, p, k_ms, W, rows, SPP, config):
+    """k_render against the FP32 VALU roof: exact reference-semantics test
+    count of this rank's launch (separate counting launch) x 47 FLOP."""
+    from pathtracerpython_amd._abi import PT_FLAG_COUNT, make_params
+    pc = make_params(p.width, p.height, p.spp, p.bounces, p.seed, p.flags | PT_FLAG_COUNT,
+                     p.rr_depth, p.row_begin, p.row_end, p.row_step, p.row_phase, p.sample_begin)
+    _, st = r.render_params(pc, stats=True)
+    tests = st["closest_tests"] + st["shadow_tests"]
+    achieved = tests * FLOP_PER_TEST / (k_ms * 1e-3) / 1e12
+    traffic, tsrc = load_traffic(config)
+    return {"bound": "valu", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+            "traffic": traffic,
+            "kernel": "k_render<false,false,false>",
+            "compute_pipe": "VALU f32 (no MFMA: scalar ray-triangle tests, not a contraction)",
+            "work_per_launch": {"ray_triangle_tests": tests,
+                                "tests_per_path_sample": round(tests / (W * rows * SPP), 2),
+                                "flop_per_test": FLOP_PER_TEST,
+                                "f64_fallback_tests": st["f64_fallbacks"],
+                                "f64_rescans": st["f64_rescans"]},
+            "kernel_ms_mean": round(k_ms, 4),
+            "hbm_frac": (round(traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
+                         if traffic else None),
+            "traffic_source": tsrc, "kernel_source_sha": source_sha()}
+
+
+def k5_roofline(r, p, render_ms):
+    """The wavefront render's dominant kernel (the shadow walks, k_wf_shadow)
+    against HBM: algorithmic bytes of its launches (counting launch) over
+    their HIP-event time (a profiling launch of the production kernels)."""
+    from pathtracerpython_amd._abi import PT_FLAG_KERNEL_TIMES, PT_FLAG_WALK_COUNT, make_params
+
+    def with_flags(f):
+        return make_params(p.width, p.height, p.spp, p.bounces, p.seed, p.flags | f, p.rr_depth,
+                           p.row_begin, p.row_end, p.row_step, p.row_phase, p.sample_begin)
+    _, wc = r.render_params(with_flags(PT_FLAG_WALK_COUNT), stats=True)
+    _, kt = r.render_params(with_flags(PT_FLAG_KERNEL_TIMES), stats=True)
+    nl = max(1, kt["shadow_launches"])
+    sh_bytes = (wc["shadow_node_visits"] * QNODE_B + wc["shadow_leaf_units"] * UNITC_B +
+                wc["shadow_queries"] * (SHADOWQ_B + SHADOW_RES_B))
+    per_launch = sh_bytes / nl
+    launch_ms = kt["shadow_ms"] / nl
+    achieved = per_launch / (launch_ms * 1e-3) / 1e9
+    traffic, tsrc = load_traffic("k5")
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "k_wf_shadow<true,false> (persistent shadow walks)",
+            "note": "latency-bound pointer chasing over an L2-resident BVH; HBM is the nearest "
+                    "physical roof for its algorithmic bytes",
+            "work_per_launch": {"queries": wc["shadow_queries"] / nl,
+                                "node_visits": wc["shadow_node_visits"] / nl,
+                                "leaf_unit_tests": wc["shadow_leaf_units"] / nl,
+                                "bytes": per_launch,
+                                "bytes_model": f"{QNODE_B} B per 4-wide node visit + {UNITC_B} B "
+                                               f"per leaf unit + {SHADOWQ_B}+{SHADOW_RES_B} B "
+                                               f"per query"},
+            "kernel_ms_mean": round(launch_ms, 4), "launches_per_render": nl,
+            "render_ms_mean": round(render_ms, 3),
+            "kernel_ms_per_render": {"shade": round(kt["shade_ms"], 2),
+                                     "shadow": round(kt["shadow_ms"], 2),
+                                     "closest": round(kt["closest_ms"], 2)},
+            "closest_walk": {"queries": wc["closest_queries"],
+                             "node_visits": wc["closest_node_visits"],
+                             "leaf_unit_tests": wc["closest_leaf_units"]},
+            "traffic_source": tsrc, "kernel_source_sha": source_sha()}
+
+
+def cpu_baseline(oracle, packed, W, H, SPP, B, config):
+    """The C oracle on this host's CPU share, on a bounded sample (~5-30 s)."""
+    import numpy as np
+    threads = oracle.host_threads()
+    if config == "k2":
+        pix = np.arange(W * H, dtype=np.int64)
+        sample = f"the whole {W}x{H} {SPP} spp {B}-bounce job"
+    elif config == "k4":
+        rows = list(range(0, H, 64))
+        pix = np.array([ix * H + iy for iy in rows for ix in range(0, W, 4)], dtype=np.int64)
+        sample = f"{len(pix)} pixels (every 4th column of every 64th row) at {SPP} spp"
+    else:
+        rs = np.random.RandomState(1)
+        pix = np.sort(rs.choice(W * H, 24, replace=False)).astype(np.int64)
+        sample = f"24 random pixels at {SPP} spp (brute force over all triangles, as the reference)"
+    t1 = time.perf_counter()
+    oracle.render(packed, W, H, SPP, B, SEED, pixels=pix, threads=threads)
+    cdt = time.perf_counter() - t1
+    return {"value": round(len(pix) * SPP / cdt / 1e6, 4), "unit": "Mpath-samples/s",
+            "cores": threads, "kind": "port",
+            "host_cpus_visible": len(os.sched_getaffinity(0)),
+            "sample": f"oracle/pt_oracle.c (f64 C restatement of main.py:186-280) on {sample}: "
+                      f"{len(pix) * SPP} path samples in {cdt:.1f} s on {threads} threads "
+                      f"(this GPU's CPU share: OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')})"}
 
 
 if __name__ == "__main__":

@@ -17,7 +17,10 @@
  * PT_E* code on failure; pt_last_error() gives a thread-local message.  Input
  * arrays are caller-owned and read-only; the library copies what it needs to
  * device memory at pt_scene_create.  Output buffers are caller-allocated.
- * A pt_scene handle is not re-entrant (one call at a time per handle).
+ * A pt_scene handle is not re-entrant (one call at a time per handle); the
+ * library orders the launches made on one handle (each waits on the GPU for
+ * the previous one, whatever stream either was issued on), because they share
+ * the handle's device scratch.
  */
 #ifndef PT_CAPI_H
 #define PT_CAPI_H
@@ -28,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 1
+#define PT_API_VERSION 2
 
 /* error codes */
 #define PT_OK 0
@@ -48,6 +51,12 @@ extern "C" {
 #define PT_FLAG_MEGAKERNEL (1u << 4)   /* scenes with a BVH: render with the
                                           single kernel instead of the
                                           wavefront kernels (same result) */
+#define PT_FLAG_WALK_COUNT (1u << 5)   /* wavefront renders (BVH scenes): count
+                                          the walks' queries, node visits and
+                                          leaf-unit tests into pt_stats
+                                          (counting kernels; synchronous)  */
+#define PT_FLAG_KERNEL_TIMES (1u << 6) /* wavefront renders: per-kernel HIP-event
+                                          times into pt_stats (synchronous) */
 
 /*
  * Flattened scene, as produced by scene_reader.Scene
@@ -103,6 +112,14 @@ typedef struct pt_stats {
     uint64_t escapes;
     uint64_t f64_fallbacks;   /* single tests re-evaluated in f64 (filter)   */
     uint64_t f64_rescans;     /* closest-hit queries re-run fully in f64     */
+    /* PT_FLAG_WALK_COUNT (wavefront renders of BVH scenes): the walk kernels'
+     * work — queries taken, 4-wide node visits, BVH leaf units tested      */
+    uint64_t shadow_queries, shadow_node_visits, shadow_leaf_units;
+    uint64_t closest_queries, closest_node_visits, closest_leaf_units;
+    /* PT_FLAG_KERNEL_TIMES (wavefront renders): summed HIP-event time (ms)
+     * and launch count of each wavefront kernel                            */
+    double shade_ms, shadow_ms, closest_ms;
+    uint64_t shade_launches, shadow_launches, closest_launches;
 } pt_stats;
 
 typedef struct pt_scene pt_scene;
@@ -116,6 +133,8 @@ int pt_device_count(int32_t* count);
 /* Upload a scene to the current HIP device.  Replaces Scene(path)'s role as
  * the thing the workers receive by pickle (main.py:201, :219). */
 int pt_scene_create(const pt_scene_desc* desc, pt_scene** out);
+/* Same, on HIP device `device` (the current device is left unchanged). */
+int pt_scene_create_on(const pt_scene_desc* desc, int32_t device, pt_scene** out);
 void pt_scene_destroy(pt_scene* scene);
 
 /* Number of rows a launch with these params renders. */
@@ -132,6 +151,20 @@ int pt_render_device(pt_scene* scene, const pt_render_params* p,
 /* Same, synchronous, with a host output buffer (rows*width*3 elements). */
 int pt_render(pt_scene* scene, const pt_render_params* p, void* out_rgb_host,
               pt_stats* stats);
+
+/* Several GPUs from one process (SURVEY.md §8(b) pt_render_multi; the
+ * reference's only parallelism is its process pool over rays,
+ * main.py:197-231).  scenes[i] is a handle of the same scene created on its
+ * own device (pt_scene_create_on).  The rows row_begin <= iy < row_end of p
+ * (p->row_step must be 1) are dealt out interleaved: handle i renders the
+ * rows with (iy - row_begin) % n == i, all devices concurrently, and each
+ * band is copied with one strided device-to-host copy straight into its rows
+ * of out_rgb_host ((row_end-row_begin) x width x 3, the layout pt_render
+ * writes for the whole range).  Bit-identical to pt_render of the same range
+ * on one device.  Synchronous.  stats (optional) receives the per-device sums
+ * (PT_FLAG_COUNT renders then run one device at a time). */
+int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* p,
+                    void* out_rgb_host, pt_stats* stats);
 
 /* Kernel time (ms) of the last pt_render_device launch on this handle. */
 int pt_last_kernel_ms(pt_scene* scene, float* ms);

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pt_capi.h (structs, flags, error codes)."""
 import ctypes as C
 
-PT_API_VERSION = 1
+PT_API_VERSION = 2
 
 PT_OK = 0
 PT_EINVAL = -1
@@ -14,6 +14,8 @@ PT_FLAG_FORCE_F64 = 1 << 1
 PT_FLAG_COUNT = 1 << 2
 PT_FLAG_OUT_F64 = 1 << 3
 PT_FLAG_MEGAKERNEL = 1 << 4
+PT_FLAG_WALK_COUNT = 1 << 5
+PT_FLAG_KERNEL_TIMES = 1 << 6
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
@@ -53,10 +55,20 @@ class PtMesh(C.Structure):
 class PtStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "closest_tests", "shadow_tests", "ray_bounces", "shading_points",
-        "light_hits", "escapes", "f64_fallbacks", "f64_rescans")]
+        "light_hits", "escapes", "f64_fallbacks", "f64_rescans",
+        "shadow_queries", "shadow_node_visits", "shadow_leaf_units",
+        "closest_queries", "closest_node_visits", "closest_leaf_units")] + \
+        [(n, C.c_double) for n in ("shade_ms", "shadow_ms", "closest_ms")] + \
+        [(n, C.c_uint64) for n in ("shade_launches", "shadow_launches", "closest_launches")]
 
-    def as_dict(self):
-        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+    COUNTERS = ("closest_tests", "shadow_tests", "ray_bounces", "shading_points",
+                "light_hits", "escapes", "f64_fallbacks", "f64_rescans")
+
+    def as_dict(self, all_fields=False):
+        """The reference-semantics counters (PT_FLAG_COUNT); all_fields adds
+        the wavefront walk counts and per-kernel times."""
+        names = [n for n, _ in self._fields_] if all_fields else self.COUNTERS
+        return {n: (float if n.endswith("_ms") else int)(getattr(self, n)) for n in names}
 
 
 def make_params(width, height, spp, bounces, seed, flags=0, rr_depth=3,

@@ -28,6 +28,9 @@ def _bind(lib):
         "pt_last_error": ([], C.c_char_p),
         "pt_device_count": ([ip], C.c_int),
         "pt_scene_create": ([C.POINTER(PtSceneDesc), C.POINTER(vp)], C.c_int),
+        "pt_scene_create_on": ([C.POINTER(PtSceneDesc), C.c_int32, C.POINTER(vp)], C.c_int),
+        "pt_render_multi": ([C.POINTER(vp), C.c_int32, C.POINTER(PtRenderParams), vp,
+                             C.POINTER(PtStats)], C.c_int),
         "pt_scene_destroy": ([vp], None),
         "pt_band_rows": ([C.POINTER(PtRenderParams), ip], C.c_int),
         "pt_render_device": ([vp, C.POINTER(PtRenderParams), vp, vp, C.POINTER(PtStats)], C.c_int),
@@ -40,11 +43,7 @@ def _bind(lib):
         "pt_obj_load": ([C.c_char_p, C.POINTER(C.POINTER(PtMesh))], C.c_int),
         "pt_mesh_free": ([C.POINTER(PtMesh)], None),
     }
-    # PT_DEV_OLD_LIB=1 (dev sweeps only): bind what an older build exports
-    lenient = os.environ.get("PT_DEV_OLD_LIB") == "1"
     for name, (args, res) in sig.items():
-        if lenient and not hasattr(lib, name):
-            continue
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
@@ -52,8 +51,8 @@ def _bind(lib):
 
 
 EXPORTS = ("pt_api_version", "pt_last_error", "pt_device_count", "pt_scene_create",
-           "pt_scene_destroy", "pt_band_rows", "pt_render_device", "pt_render",
-           "pt_last_kernel_ms", "pt_intersect_objects", "pt_compute_color",
+           "pt_scene_create_on", "pt_render_multi", "pt_scene_destroy", "pt_band_rows",
+           "pt_render_device", "pt_render", "pt_last_kernel_ms", "pt_intersect_objects", "pt_compute_color",
            "pt_image_u8_device", "pt_image_u8", "pt_obj_load", "pt_mesh_free")
 
 
@@ -71,7 +70,12 @@ def lib():
         import torch  # noqa: F401  (shares libamdhip64 with torch)
     except Exception:
         pass
-    _lib = _bind(C.CDLL(LIB_PATH))
+    lib_ = _bind(C.CDLL(LIB_PATH))
+    from ._abi import PT_API_VERSION
+    if lib_.pt_api_version() != PT_API_VERSION:
+        raise NativeError(f"{LIB_PATH} has C-ABI version {lib_.pt_api_version()}, this binding "
+                          f"needs {PT_API_VERSION}: rebuild it (python __graft_entry__.py build)")
+    _lib = lib_
     return _lib
 
 

@@ -14,6 +14,7 @@
 
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "pt_path.h"
 #include "pt_wavefront.h"
@@ -245,11 +246,30 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
 #define PT_WALK_WAVES 1
 #endif
 constexpr int kWalkStack = 32;   // entries of a walk kernel's shared-memory stack
-template <bool UC>
+// COUNT (PT_FLAG_WALK_COUNT launches only): per-query work of the walk —
+// queries, 4-wide node visits, leaf-unit tests — summed into wc[0..2]
+// (the walks' algorithmic bytes).
+template <bool COUNT>
+__device__ __forceinline__ void flush_walk_counts(uint32_t q, uint32_t nodes, uint32_t units,
+                                                  unsigned long long* wc) {
+    if (!COUNT) return;
+    uint32_t v[3] = {q, nodes, units};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        uint32_t x = v[i];
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&wc[i], (unsigned long long)x);
+    }
+}
+__device__ __forceinline__ uint32_t leaf_units(int ref) { return (uint32_t)(~ref) & 7u; }
+
+template <bool UC, bool COUNT>
 __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPath* __restrict__ W,
                                                    WfShadowQ* __restrict__ SQ,
                                                    const int32_t* __restrict__ list, int32_t* counters,
-                                                   int32_t thr) {
+                                                   int32_t thr, unsigned long long* wc) {
+    uint32_t c_q = 0, c_nodes = 0, c_units = 0;
     const int32_t count = counters[0];
     int32_t slot = -1;
     bool exhausted = false;
@@ -269,6 +289,7 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
             if (need) {
                 if (i < count) {
                     slot = list[i];
+                    if (COUNT) ++c_q;
                     F3 o32;
                     int ogrp;
                     wf_get_shadow(S, SQ[slot], &o32, &ogrp, &sh);
@@ -292,10 +313,16 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
             const int32_t nd = (int32_t)__popcll(__ballot(desc));
             // end it early only when some lane has a leaf to test (progress)
             if (nd == 0 || (nd <= thr && __any(slot >= 0 && (pl != kNoRef || T.ref <= -2)))) break;
-            if (desc) strav_qnode<false>(T, K, S, &sh);
+            if (desc) {
+                if (COUNT) ++c_nodes;
+                strav_qnode<false>(T, K, S, &sh);
+            }
         }
         if (slot >= 0) {
             const Spill sp{W[slot].sp, 1};
+            if (COUNT)
+                c_units += (pl != kNoRef ? leaf_units(pl) : 0u) + (pl2 != kNoRef ? leaf_units(pl2) : 0u) +
+                           (T.ref <= -2 ? leaf_units(T.ref) : 0u);
             if (pl != kNoRef) strav_units<false, UC>(T, S, &sh, sp, nullptr, pl, plr);
             if (pl2 != kNoRef) strav_units<false, UC>(T, S, &sh, sp, nullptr, pl2, plr2);
             pl = pl2 = kNoRef;
@@ -310,13 +337,15 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
             slot = -1;
         }
     }
+    flush_walk_counts<COUNT>(c_q, c_nodes, c_units, wc);
 }
 
-template <bool UC>
+template <bool UC, bool COUNT>
 __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
                                                     WfClosestQ* __restrict__ CQ,
                                                     const int32_t* __restrict__ list, int32_t* counters,
-                                                    int32_t thr) {
+                                                    int32_t thr, unsigned long long* wc) {
+    uint32_t c_q = 0, c_nodes = 0, c_units = 0;
     const int32_t count = counters[0];   // [count, head]
     int32_t slot = -1;
     bool exhausted = false;
@@ -335,6 +364,7 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfP
             if (need) {
                 if (i < count) {
                     slot = list[i];
+                    if (COUNT) ++c_q;
                     const WfClosestQ q = CQ[slot];
                     ca = wf_get_acc(q);
                     ctrav_init(T, S, F3{q.o[0], q.o[1], q.o[2]}, q.ogrp, F3{q.d[0], q.d[1], q.d[2]},
@@ -354,10 +384,16 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfP
             const bool desc = slot >= 0 && T.ref >= 0;
             const int32_t nd = (int32_t)__popcll(__ballot(desc));
             if (nd == 0 || (nd <= thr && __any(slot >= 0 && (pl != kNoRef || T.ref <= -2)))) break;
-            if (desc) ctrav_qnode(T, K, S, &ca);
+            if (desc) {
+                if (COUNT) ++c_nodes;
+                ctrav_qnode(T, K, S, &ca);
+            }
         }
         if (slot >= 0) {
             const Spill sp{W[slot].sp, 1};
+            if (COUNT)
+                c_units += (pl != kNoRef ? leaf_units(pl) : 0u) + (pl2 != kNoRef ? leaf_units(pl2) : 0u) +
+                           (T.ref <= -2 ? leaf_units(T.ref) : 0u);
             if (pl != kNoRef) ctrav_units<false, UC>(T, S, &ca, sp, nullptr, pl);
             if (pl2 != kNoRef) ctrav_units<false, UC>(T, S, &ca, sp, nullptr, pl2);
             pl = pl2 = kNoRef;
@@ -371,6 +407,7 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfP
             slot = -1;
         }
     }
+    flush_walk_counts<COUNT>(c_q, c_nodes, c_units, wc);
 }
 
 __global__ __launch_bounds__(256) void k_wf_final(SceneK S, RenderK R, const WfPath* __restrict__ W,
@@ -438,6 +475,7 @@ struct pt_scene {
     size_t wf_slots = 0;
     hipStream_t wf_side = nullptr;             // the closest walks run beside the shadow walks
     hipEvent_t wf_ev_shade = nullptr, wf_ev_walk = nullptr;
+    std::vector<hipEvent_t> prof_ev;           // PT_FLAG_KERNEL_TIMES
 };
 
 namespace {
@@ -503,11 +541,25 @@ void pt_scene_destroy(pt_scene* s) {
         if (s->wf_ev_shade) (void)hipEventDestroy(s->wf_ev_shade);
         if (s->wf_ev_walk) (void)hipEventDestroy(s->wf_ev_walk);
         if (s->wf_side) (void)hipStreamDestroy(s->wf_side);
+        for (hipEvent_t e : s->prof_ev) (void)hipEventDestroy(e);
         if (s->ev0) (void)hipEventDestroy(s->ev0);
         if (s->ev1) (void)hipEventDestroy(s->ev1);
         if (s->stream) (void)hipStreamDestroy(s->stream);
     }
     delete s;
+}
+
+int pt_scene_create_on(const pt_scene_desc* desc, int32_t device, pt_scene** out) {
+    if (!out) return fail(PT_EINVAL, "null output handle");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(PT_ENODEV, "no HIP device visible (the MI355X path needs a gfx950 GPU)");
+    if (device < 0 || device >= ndev)
+        return fail(PT_EINVAL, "device " + std::to_string(device) + " out of range (" +
+                                   std::to_string(ndev) + " visible)");
+    DeviceGuard g(device);
+    return pt_scene_create(desc, out);
 }
 
 int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
@@ -647,7 +699,8 @@ static uint32_t choose_split(uint64_t image_pixels, int32_t spp, bool bvh) {
 // queries it appended.  A slot runs at most n_samples x bounces bounces plus
 // the primary ray, so that many steps (+1 to finish the last bounce) drain
 // every slot; steps after that would find no work.
-static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_dev, hipStream_t st) {
+static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_dev, hipStream_t st,
+                            uint32_t flags, pt_stats* stats) {
     const size_t slots = (size_t)grid.x * 256;
     const size_t sz_w = slots * sizeof(WfPath), sz_s = slots * sizeof(WfShadowQ),
                  sz_c = slots * sizeof(WfClosestQ), sz_l = 2 * slots * sizeof(int32_t);
@@ -675,29 +728,61 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
         std::max(1u, std::min<unsigned>(grid.x, (unsigned)PT_WF_BLOCKS_PER_CU * (unsigned)s->n_cu));
     const int32_t per_slot = (R.spp + (int32_t)R.split - 1) / (int32_t)R.split;
     const int32_t steps = per_slot * R.bounces + 2;
+    const bool wcount = (flags & PT_FLAG_WALK_COUNT) != 0 && stats;
+    const bool times = (flags & PT_FLAG_KERNEL_TIMES) != 0 && stats;
+    unsigned long long* wc = (unsigned long long*)s->stats;   // [0..2] shadow, [3..5] closest
+    if (wcount) HIPCHK(hipMemsetAsync(s->stats, 0, sizeof(StatsDev), st));
+    // per-kernel HIP events (PT_FLAG_KERNEL_TIMES): shade, shadow, closest x (start, end) per step
+    if (times) {
+        const size_t ne = (size_t)steps * 6;
+        while (s->prof_ev.size() < ne) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            s->prof_ev.push_back(e);
+        }
+    }
+    auto mark = [&](int32_t step, int k, int end, hipStream_t on) -> hipError_t {
+        return times ? hipEventRecord(s->prof_ev[(size_t)step * 6 + k * 2 + end], on) : hipSuccess;
+    };
+    auto closest_walk = [&](hipStream_t on) {
+        const int32_t* l = lists + slots;
+        if (s->dev.bunitc) {
+            if (wcount) hipLaunchKernelGGL((k_wf_closest<true, true>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3);
+            else hipLaunchKernelGGL((k_wf_closest<true, false>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3);
+        } else {
+            if (wcount) hipLaunchKernelGGL((k_wf_closest<false, true>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3);
+            else hipLaunchKernelGGL((k_wf_closest<false, false>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3);
+        }
+    };
+    auto shadow_walk = [&](hipStream_t on) {
+        const int32_t* l = lists;
+        if (s->dev.bunitc) {
+            if (wcount) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc);
+            else hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc);
+        } else {
+            if (wcount) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc);
+            else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc);
+        }
+    };
     HIPCHK(hipEventRecord(s->ev0, st));
     for (int32_t step = 0; step < steps; ++step) {
         HIPCHK(hipMemsetAsync(counters, 0, 4 * sizeof(int32_t), st));
+        HIPCHK(mark(step, 0, 0, st));
         hipLaunchKernelGGL(k_wf_shade, grid, dim3(256), 0, st, s->dev, R, step, W, SQ, CQ, lists,
                            counters, (uint32_t)slots);
+        HIPCHK(mark(step, 0, 1, st));
         if (step + 1 < steps) {
             // the two walks only read the shade step's output and write
             // disjoint records: the closest walks run on a side stream
             HIPCHK(hipEventRecord(s->wf_ev_shade, st));
             HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
-            if (s->dev.bunitc)
-                hipLaunchKernelGGL(k_wf_closest<true>, dim3(wf_blocks), dim3(256), 0, s->wf_side, s->dev,
-                                   W, CQ, (const int32_t*)(lists + slots), counters + 2, PT_WF_THR_CLOSEST);
-            else
-                hipLaunchKernelGGL(k_wf_closest<false>, dim3(wf_blocks), dim3(256), 0, s->wf_side, s->dev,
-                                   W, CQ, (const int32_t*)(lists + slots), counters + 2, PT_WF_THR_CLOSEST);
+            HIPCHK(mark(step, 2, 0, s->wf_side));
+            closest_walk(s->wf_side);
+            HIPCHK(mark(step, 2, 1, s->wf_side));
             HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
-            if (s->dev.bunitc)
-                hipLaunchKernelGGL(k_wf_shadow<true>, dim3(wf_blocks), dim3(256), 0, st, s->dev, W, SQ,
-                                   (const int32_t*)lists, counters, PT_WF_THR_SHADOW);
-            else
-                hipLaunchKernelGGL(k_wf_shadow<false>, dim3(wf_blocks), dim3(256), 0, st, s->dev, W, SQ,
-                                   (const int32_t*)lists, counters, PT_WF_THR_SHADOW);
+            HIPCHK(mark(step, 1, 0, st));
+            shadow_walk(st);
+            HIPCHK(mark(step, 1, 1, st));
             HIPCHK(hipStreamWaitEvent(st, s->wf_ev_walk, 0));
         }
     }
@@ -705,6 +790,35 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(s->ev1, st));
     s->timed = true;
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        if (wcount || times) HIPCHK(hipStreamSynchronize(st));
+        if (wcount) {
+            StatsDev h;
+            HIPCHK(hipMemcpy(&h, s->stats, sizeof(h), hipMemcpyDeviceToHost));
+            stats->shadow_queries = h.v[0];
+            stats->shadow_node_visits = h.v[1];
+            stats->shadow_leaf_units = h.v[2];
+            stats->closest_queries = h.v[3];
+            stats->closest_node_visits = h.v[4];
+            stats->closest_leaf_units = h.v[5];
+        }
+        if (times) {
+            double t[3] = {0, 0, 0};
+            uint64_t n[3] = {0, 0, 0};
+            for (int32_t step = 0; step < steps; ++step)
+                for (int k = 0; k < 3; ++k) {
+                    if (k > 0 && step + 1 >= steps) continue;
+                    float ms = 0.f;
+                    HIPCHK(hipEventElapsedTime(&ms, s->prof_ev[(size_t)step * 6 + k * 2],
+                                               s->prof_ev[(size_t)step * 6 + k * 2 + 1]));
+                    t[k] += ms;
+                    ++n[k];
+                }
+            stats->shade_ms = t[0]; stats->shadow_ms = t[1]; stats->closest_ms = t[2];
+            stats->shade_launches = n[0]; stats->shadow_launches = n[1]; stats->closest_launches = n[2];
+        }
+    }
     return PT_OK;
 }
 
@@ -776,11 +890,7 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     const bool wavefront = s->dev.n_bnode > 0 && !count && !f64 &&
                            !(p->flags & PT_FLAG_MEGAKERNEL) && s->dev.n_qnode > 0 &&
                            s->dev.qstack <= kWalkStack;
-    if (wavefront) {
-        rc = render_wavefront(s, R, grid, out_dev, st);
-        if (!rc && stats) memset(stats, 0, sizeof(*stats));
-        return rc;
-    }
+    if (wavefront) return render_wavefront(s, R, grid, out_dev, st, p->flags, stats);
     if (count) HIPCHK(hipMemsetAsync(s->stats, 0, sizeof(StatsDev), st));
     HIPCHK(hipEventRecord(s->ev0, st));
     if (f64) {
@@ -837,6 +947,74 @@ int pt_render(pt_scene* s, const pt_render_params* p, void* out_host, pt_stats* 
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(out_host, s->out_dev, bytes, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
+    return PT_OK;
+}
+
+int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* p, void* out_host,
+                    pt_stats* stats) {
+    if (!scenes || n <= 0) return fail(PT_EINVAL, "need n >= 1 scene handles");
+    for (int32_t i = 0; i < n; ++i)
+        if (!scenes[i]) return fail(PT_EINVAL, "null scene handle");
+    int rc = validate(p);
+    if (rc) return rc;
+    if (p->row_step != 1) return fail(PT_EINVAL, "pt_render_multi deals out the rows itself: row_step must be 1");
+    int32_t first = 0, total = 0;
+    band_layout(p, &first, &total);
+    if (total == 0) return PT_OK;
+    if (!out_host) return fail(PT_EINVAL, "null output");
+    const int32_t rb = first, re = first + total;   // the rows, clamped to the image
+    const size_t elem = (p->flags & PT_FLAG_OUT_F64) ? sizeof(double) : sizeof(float);
+    const size_t row_bytes = (size_t)p->width * 3 * elem;
+    const bool count = (p->flags & PT_FLAG_COUNT) != 0;
+    if (stats) memset(stats, 0, sizeof(*stats));
+    std::vector<pt_render_params> bp(n);
+    std::vector<int32_t> rows(n, 0);
+    // 1. every device renders its band into its staging buffer (asynchronous)
+    for (int32_t i = 0; i < n; ++i) {
+        pt_scene* s = scenes[i];
+        bp[i] = *p;
+        bp[i].row_begin = rb;
+        bp[i].row_end = re;
+        bp[i].row_step = n;
+        bp[i].row_phase = (rb + i) % n;
+        int32_t f = 0;
+        band_layout(&bp[i], &f, &rows[i]);
+        if (rows[i] == 0) continue;
+        DeviceGuard g(s->device);
+        const size_t bytes = (size_t)rows[i] * row_bytes;
+        if (bytes > s->out_cap) {
+            if (s->out_dev) (void)hipFree(s->out_dev);
+            s->out_dev = nullptr;
+            s->out_cap = 0;
+            HIPCHK(hipMalloc(&s->out_dev, bytes));
+            s->out_cap = bytes;
+        }
+        pt_stats st;
+        rc = pt_render_device(s, &bp[i], s->out_dev, s->stream, (count && stats) ? &st : nullptr);
+        if (rc) return rc;
+        if (count && stats) {
+            uint64_t* dst = &stats->closest_tests;
+            const uint64_t* src = &st.closest_tests;
+            for (int k = 0; k < 8; ++k) dst[k] += src[k];
+        }
+    }
+    // 2. each band lands in its rows of the host frame: band row j (launch
+    // order, highest iy first) is frame row (re-1-iy) = (re-1-iy_top) + j*n
+    for (int32_t i = 0; i < n; ++i) {
+        if (rows[i] == 0) continue;
+        pt_scene* s = scenes[i];
+        DeviceGuard g(s->device);
+        const int32_t phase = bp[i].row_phase;
+        int32_t iy_top = re - 1;
+        while (((iy_top % n) + n) % n != phase) --iy_top;
+        char* dst = (char*)out_host + (size_t)(re - 1 - iy_top) * row_bytes;
+        HIPCHK(hipMemcpy2DAsync(dst, (size_t)n * row_bytes, s->out_dev, row_bytes, row_bytes,
+                                (size_t)rows[i], hipMemcpyDeviceToHost, s->stream));
+    }
+    for (int32_t i = 0; i < n; ++i) {
+        DeviceGuard g(scenes[i]->device);
+        HIPCHK(hipStreamSynchronize(scenes[i]->stream));
+    }
     return PT_OK;
 }
 

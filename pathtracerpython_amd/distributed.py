@@ -57,6 +57,17 @@ def gather_tiles(tile, group=None):
     return bufs
 
 
+def deinterleave(gathered, out):
+    """Frame from the gathered row tiles of an interleaved split whose height
+    is a multiple of the world size, as one tensor copy (on the tiles'
+    device): gathered (world, rows, W, 3), tile r row j (top-first) = image
+    row iy = r + world*(rows-1-j) = frame row world*j + (world-1-r).  out:
+    (world*rows, W, 3)."""
+    world, rows = gathered.shape[0], gathered.shape[1]
+    out.view(rows, world, *gathered.shape[2:]).copy_(gathered.flip(0).permute(1, 0, 2, 3))
+    return out
+
+
 def render_distributed(renderer, width, height, spp=1, bounces=1, seed=None, rr=False,
                        rr_depth=3, group=None, return_tiles=False):
     """Render `height` rows interleaved over the ranks of `group` on each

@@ -6,7 +6,8 @@
 Same positional scene argument and flags (-r spp, -b bounces, --out,
 --show-img); the whole spp x bounce loop runs on the GPU (render.py).  Extra
 flags of this build: --seed (RNG key; default the SDL `seed`), --rr
-(Russian roulette), --size W H (override the SDL size), --devices.  The
+(Russian roulette), --size W H (override the SDL size), --devices N (N GPUs:
+one rank process per GPU, rows interleaved, one RCCL gather; launch.py).  The
 reference's interactive 3-D viewer flags (--show-scene, --show-normals,
 --show-screen, --show-inter -> plot.py) are accepted and ignored with a
 notice: the pyqtgraph viewer is out of scope.
@@ -33,14 +34,63 @@ def setup(argv=None):
     parser.add_argument('--size', type=int, nargs=2, metavar=('W', 'H'), default=None)
     parser.add_argument('--save-raw', default=None,
                         help='also save the float framebuffer (.npy, before normalisation)')
+    parser.add_argument('--devices', type=int, default=1,
+                        help='GPUs: one rank process each (torch.distributed over RCCL); '
+                             'started here unless already under torch.distributed.run')
     return parser.parse_args(argv)
+
+
+def render_ranks(scene, args, W, H):
+    """This rank's band (rows iy % world == rank) into a device tile, one
+    RCCL gather to rank 0, the frame assembled there.  Returns (image array
+    or None, f64 framebuffer) on rank 0, (None, None) elsewhere."""
+    import torch
+    import torch.distributed as dist
+    from .distributed import assemble, deinterleave, gather_tiles, max_band_rows
+    from .launch import rank_env
+    from .render import Renderer, image_u8, image_u8_device
+    rank, local, world = rank_env()
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    try:
+        with Renderer(scene) as r:
+            p = r.params(W, H, args.n_rays, args.n_bounces, args.seed, args.rr, out_f64=True,
+                         row_step=world, row_phase=rank)
+            tile = torch.zeros((max_band_rows(H, world), W, 3), dtype=torch.float64, device="cuda")
+            s = torch.cuda.current_stream().cuda_stream
+            r.render_device(p, tile.data_ptr(), s)
+            tiles = gather_tiles(tile)
+            if rank == 0:
+                print(f'render: {W}x{H}, {args.n_rays} spp, {args.n_bounces} bounces on {world} '
+                      f'GPUs, rank-0 kernel {r.last_kernel_ms():.3f} ms')
+        if rank != 0:
+            return None, None
+        if H % world == 0:
+            frame = deinterleave(torch.stack(tiles), torch.empty((H, W, 3), dtype=torch.float64,
+                                                                 device="cuda"))
+            arr = None
+            if W == H:
+                img = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+                image_u8_device(frame.data_ptr(), W, H, True, img.data_ptr(),
+                                torch.cuda.current_stream().cuda_stream)
+                arr = img.cpu().numpy()
+            return arr, frame.cpu().numpy()
+        fb = assemble([t.cpu().numpy() for t in tiles], H)
+        return (image_u8(fb) if W == H else None), fb
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main(argv=None):
     args = setup(argv)
+    from .launch import rank_env, spawn_ranks, under_launcher
+    if args.devices > 1 and not under_launcher():
+        # one fresh process per GPU; this parent never touches the GPU
+        raise SystemExit(spawn_ranks(args.devices, ['-m', 'pathtracerpython_amd.main'] +
+                                     list(sys.argv[1:] if argv is None else argv)))
     from .render import Renderer
     from .scene_reader import Scene
-    from .utils import framebuffer_to_image
     scene = Scene(args.scene)
     W, H = (args.size if args.size else (scene.width, scene.height))
     print(f'Number of objects: {len(scene.objects)}')
@@ -48,6 +98,14 @@ def main(argv=None):
     if args.show_scene or args.show_normals or args.show_screen or args.show_inter:
         print('note: the 3-D scene viewer (plot.py) is not part of this build; ignoring --show-*',
               file=sys.stderr)
+    rank, _, world = rank_env()
+    if world != args.devices:
+        raise SystemExit(f'--devices {args.devices} but WORLD_SIZE={world}')
+    if world > 1:
+        arr, fb = render_ranks(scene, args, W, H)
+        if rank != 0:
+            return None
+        return finish(args, arr, fb)
     with Renderer(scene) as r:
         if W == H:   # make_image on the device (utils.py:150-161)
             arr, fb = r.render_image(W, H, spp=args.n_rays, bounces=args.n_bounces,
@@ -58,6 +116,12 @@ def main(argv=None):
             arr = None
         print(f'render: {W}x{H}, {args.n_rays} spp, {args.n_bounces} bounces, '
               f'kernel {r.last_kernel_ms():.3f} ms')
+    return finish(args, arr, fb)
+
+
+def finish(args, arr, fb):
+    """--save-raw / --out / --show-img of a rendered frame (rank 0)."""
+    from .utils import framebuffer_to_image
     if args.save_raw:
         np.save(args.save_raw, fb)
     if arr is not None:

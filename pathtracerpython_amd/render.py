@@ -17,8 +17,8 @@ import ctypes as C
 import numpy as np
 
 from . import _native
-from ._abi import (PT_FLAG_COUNT, PT_FLAG_FORCE_F64, PT_FLAG_MEGAKERNEL, PT_FLAG_OUT_F64, PT_FLAG_RR, PtStats,
-                   band_rows, make_params)
+from ._abi import (PT_FLAG_COUNT, PT_FLAG_FORCE_F64, PT_FLAG_KERNEL_TIMES, PT_FLAG_MEGAKERNEL,
+                   PT_FLAG_OUT_F64, PT_FLAG_RR, PT_FLAG_WALK_COUNT, PtStats, band_rows, make_params)
 from .pack import pack_scene
 
 _dp = C.POINTER(C.c_double)
@@ -26,30 +26,40 @@ _ip = C.POINTER(C.c_int32)
 
 
 class Renderer:
-    """A scene uploaded to the current HIP device (one `pt_scene` handle)."""
+    """A scene uploaded to a HIP device (one `pt_scene` handle): the current
+    device, or `device`."""
 
-    def __init__(self, scene):
+    def __init__(self, scene, device=None, packed=None):
         self.scene = scene
-        self.packed = pack_scene(scene)
+        self.packed = packed if packed is not None else pack_scene(scene)
         self._lib = _native.lib()
         h = C.c_void_p()
-        _native.check(self._lib.pt_scene_create(C.byref(self.packed.desc), C.byref(h)),
-                      "pt_scene_create")
+        if device is None:
+            _native.check(self._lib.pt_scene_create(C.byref(self.packed.desc), C.byref(h)),
+                          "pt_scene_create")
+        else:
+            _native.check(self._lib.pt_scene_create_on(C.byref(self.packed.desc), int(device),
+                                                       C.byref(h)), "pt_scene_create_on")
         self._h = h
+        self.device = device
 
     # ------------------------------------------------------------ render --
     def params(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
                rr_depth=3, force_f64=False, count=False, out_f64=False, row_begin=0,
-               row_end=None, row_step=1, row_phase=0, sample_begin=0, megakernel=False):
+               row_end=None, row_step=1, row_phase=0, sample_begin=0, megakernel=False,
+               walk_count=False, kernel_times=False):
         """megakernel=True: scenes with a BVH render with the single kernel
-        instead of the wavefront kernels (the same framebuffer, bit for bit)."""
+        instead of the wavefront kernels (the same framebuffer, bit for bit).
+        walk_count / kernel_times (wavefront renders): the walks' work counts /
+        per-kernel HIP-event times in the stats."""
         width = int(self.scene.width if width is None else width)
         height = int(self.scene.height if height is None else height)
         seed = self.scene.seed if seed is None else seed
         seed = 0 if seed is None else int(seed)
         flags = (PT_FLAG_RR if rr else 0) | (PT_FLAG_FORCE_F64 if force_f64 else 0) | \
             (PT_FLAG_COUNT if count else 0) | (PT_FLAG_OUT_F64 if out_f64 else 0) | \
-            (PT_FLAG_MEGAKERNEL if megakernel else 0)
+            (PT_FLAG_MEGAKERNEL if megakernel else 0) | \
+            (PT_FLAG_WALK_COUNT if walk_count else 0) | (PT_FLAG_KERNEL_TIMES if kernel_times else 0)
         return make_params(width, height, spp, bounces, seed, flags, rr_depth, row_begin,
                            row_end, row_step, row_phase, sample_begin)
 
@@ -65,7 +75,8 @@ class Renderer:
         st = PtStats()
         _native.check(self._lib.pt_render(self._h, C.byref(p), C.c_void_p(out.ctypes.data),
                                           C.byref(st)), "pt_render")
-        return (out, st.as_dict()) if stats else out
+        wide = bool(p.flags & (PT_FLAG_WALK_COUNT | PT_FLAG_KERNEL_TIMES))
+        return (out, st.as_dict(all_fields=wide)) if stats else out
 
     def render(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
                rr_depth=3, force_f64=False, stats=False, out_f64=False, megakernel=False,
@@ -161,6 +172,47 @@ def render(scene, width=None, height=None, spp=1, bounces=1, seed=None, rr=False
     """main.py's render as a function: framebuffer (H, W, 3) float32."""
     with Renderer(scene) as r:
         return r.render(width, height, spp, bounces, seed, rr, rr_depth)
+
+
+class MultiRenderer:
+    """One scene on several GPUs of this process (pt_render_multi): the rows
+    are dealt out interleaved, every device renders its band concurrently and
+    each band is copied straight into its rows of the host framebuffer —
+    bit-identical to Renderer.render on one device.  (The multi-process path
+    over RCCL is distributed.py.)"""
+
+    def __init__(self, scene, devices):
+        self.devices = [int(d) for d in devices]
+        if not self.devices:
+            raise ValueError("need at least one device")
+        first = Renderer(scene, device=self.devices[0])
+        self.renderers = [first] + [Renderer(scene, device=d, packed=first.packed)
+                                    for d in self.devices[1:]]
+        self.packed = first.packed
+
+    def render(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
+               rr_depth=3, stats=False, out_f64=False, row_begin=0, row_end=None):
+        r0 = self.renderers[0]
+        p = r0.params(width, height, spp, bounces, seed, rr, rr_depth, count=stats,
+                      out_f64=out_f64, row_begin=row_begin, row_end=row_end)
+        rows = r0.band_rows(p)
+        out = np.zeros((rows, p.width, 3), dtype=np.float64 if out_f64 else np.float32)
+        hs = (C.c_void_p * len(self.renderers))(*[r._h.value for r in self.renderers])
+        st = PtStats()
+        _native.check(r0._lib.pt_render_multi(hs, len(self.renderers), C.byref(p),
+                                              C.c_void_p(out.ctypes.data), C.byref(st)),
+                      "pt_render_multi")
+        return (out, st.as_dict()) if stats else out
+
+    def close(self):
+        for r in self.renderers:
+            r.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def image_u8_device(fb_ptr, width, height, f64, out_ptr, stream=None):

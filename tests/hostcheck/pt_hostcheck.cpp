@@ -6,6 +6,7 @@
 #define __host__
 #define __device__
 #define __forceinline__ inline
+#include <cstddef>
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
@@ -22,6 +23,20 @@ extern "C" {
 
 // Render the band of p on the host with the kernel's lane code (split = 1).
 // out: rows*W*3 float64 in image orientation.  counters[8] (optional).
+// sizes and field offsets of the C-ABI structs as the C++ compiler lays
+// them out (the ctypes mirror in _abi.py must agree)
+int hc_abi_layout(int64_t* out) {
+    out[0] = (int64_t)sizeof(pt_scene_desc);
+    out[1] = (int64_t)sizeof(pt_render_params);
+    out[2] = (int64_t)sizeof(pt_stats);
+    out[3] = (int64_t)offsetof(pt_stats, shadow_queries);
+    out[4] = (int64_t)offsetof(pt_stats, shade_ms);
+    out[5] = (int64_t)offsetof(pt_stats, closest_launches);
+    out[6] = (int64_t)offsetof(pt_scene_desc, light_rgb);
+    out[7] = (int64_t)offsetof(pt_render_params, sample_begin);
+    return 0;
+}
+
 int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
               double* out, uint64_t* counters) {
     HostScene H;

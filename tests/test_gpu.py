@@ -277,3 +277,45 @@ def test_from_list_order_matches_golden_png(R):
     fb = R.render(W, H, spp, B, seed, out_f64=True)
     assert np.array_equal(np.asarray(framebuffer_to_image(fb)), g["png"])
     assert np.abs(fb - from_list_order(g["colors"], W, H)).max() <= TOL
+
+
+# ------------------------------------------- one-process multi-device --
+def test_render_multi_bands_bitwise(cornell):
+    """pt_render_multi deals the rows out interleaved over its handles and
+    copies each band into its rows of the host frame: bit-identical to one
+    render (here several handles on device 0, which exercises the dealing,
+    the strided copies and the concurrency of the handles)."""
+    from pathtracerpython_amd.render import MultiRenderer
+    W, H = 70, 53
+    with Renderer(cornell) as r:
+        ref, st = r.render(W, H, 16, 4, 3, out_f64=True, stats=True)
+        ref32 = r.render(W, H, 16, 4, 3)
+    for n in (1, 2, 3, 5):
+        with MultiRenderer(cornell, [0] * n) as m:
+            assert np.array_equal(m.render(W, H, 16, 4, 3, out_f64=True), ref)
+            assert np.array_equal(m.render(W, H, 16, 4, 3), ref32)
+    with MultiRenderer(cornell, [0, 0]) as m:
+        band = m.render(W, H, 16, 4, 3, out_f64=True, row_begin=5, row_end=40)
+        assert np.array_equal(band, ref[H - 40:H - 5])
+        _, mst = m.render(W, H, 16, 4, 3, out_f64=True, stats=True)
+        assert mst == st
+
+
+def test_wavefront_walk_counts_and_times(k5small):
+    """PT_FLAG_WALK_COUNT (counting walk kernels) and PT_FLAG_KERNEL_TIMES
+    leave the framebuffer unchanged and report plausible work (queries, node
+    visits and leaf units all present, one walk launch per shade launch but
+    the last)."""
+    with Renderer(k5small) as r:
+        ref = r.render(64, 64, 4, 4, 9, out_f64=True)
+        fb, st = r.render_params(r.params(64, 64, 4, 4, 9, out_f64=True, walk_count=True),
+                                 stats=True)
+        assert np.array_equal(fb, ref)
+        assert st["shadow_queries"] > 0 and st["closest_queries"] > 0
+        assert st["shadow_node_visits"] > 0 and st["closest_node_visits"] > 0
+        assert st["closest_leaf_units"] > 0 and st["shadow_leaf_units"] > 0
+        fb, tt = r.render_params(r.params(64, 64, 4, 4, 9, out_f64=True, kernel_times=True),
+                                 stats=True)
+        assert np.array_equal(fb, ref)
+        assert tt["shade_launches"] == tt["shadow_launches"] + 1 == tt["closest_launches"] + 1
+        assert tt["shade_ms"] > 0 and tt["shadow_ms"] > 0 and tt["closest_ms"] > 0

@@ -1,0 +1,44 @@
+"""The self-spawn multi-rank path of bench.py and the CLI (--gpus N /
+--devices N without torch.distributed.run): launch.spawn_ranks starts N fresh
+rank processes with the rendezvous in their environment; here world 2 over
+gloo on CPU, tiles from the oracle (tests/rank_worker.py), device-style
+assembly with distributed.deinterleave."""
+import os
+
+import numpy as np
+
+from conftest import ROOT
+
+
+def test_spawn_two_ranks_gloo_frame(tmp_path, packed):
+    from oracle import oracle
+    from pathtracerpython_amd.launch import spawn_ranks
+    from pathtracerpython_amd.render import from_list_order
+    W, H, spp, B, seed = 10, 12, 2, 3, 9   # H a multiple of the world size
+    out = str(tmp_path / "frame.npy")
+    rc = spawn_ranks(2, [os.path.join(ROOT, "tests", "rank_worker.py"), out,
+                         str(W), str(H), str(spp), str(B), str(seed)])
+    assert rc == 0
+    full, _ = oracle.render(packed, W, H, spp, B, seed)
+    assert np.array_equal(np.load(out), from_list_order(full, W, H))
+
+
+def test_spawn_reports_failure():
+    from pathtracerpython_amd.launch import spawn_ranks
+    assert spawn_ranks(2, ["-c", "import os, sys; sys.exit(3 if os.environ['RANK'] == '1' else 0)"]) == 3
+
+
+def test_deinterleave_matches_assemble():
+    import torch
+    from pathtracerpython_amd.distributed import assemble, deinterleave
+    rs = np.random.RandomState(0)
+    for world, rows in ((1, 5), (2, 4), (4, 3), (8, 2)):
+        g = torch.from_numpy(rs.rand(world, rows, 7, 3))
+        out = deinterleave(g, torch.empty((world * rows, 7, 3), dtype=torch.float64))
+        assert np.array_equal(out.numpy(), assemble([t.numpy() for t in g], world * rows))
+
+
+def test_cli_devices_flag_parses():
+    from pathtracerpython_amd.main import setup
+    a = setup(["scene.sdl", "--devices", "4", "-r", "8"])
+    assert a.devices == 4 and a.n_rays == 8
