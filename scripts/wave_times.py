@@ -1,5 +1,5 @@
 """Per-wave start/end clocks of one K2 launch (dev tool; needs a library built
-with the wave-time instrumentation, passed as PT_HIP_LIB with PT_DEV_OLD_LIB=1).
+with the wave-time instrumentation, passed as PT_HIP_LIB with).
 Prints the occupancy profile: how long the launch runs below full occupancy
 at its start and end.  Usage: wave_times.py [W] [spp] [waves in the launch]."""
 import ctypes as C, os, sys

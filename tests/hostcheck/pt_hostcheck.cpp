@@ -21,8 +21,6 @@ using namespace pt;
 
 extern "C" {
 
-// Render the band of p on the host with the kernel's lane code (split = 1).
-// out: rows*W*3 float64 in image orientation.  counters[8] (optional).
 // sizes and field offsets of the C-ABI structs as the C++ compiler lays
 // them out (the ctypes mirror in _abi.py must agree)
 int hc_abi_layout(int64_t* out) {
@@ -37,6 +35,8 @@ int hc_abi_layout(int64_t* out) {
     return 0;
 }
 
+// Render the band of p on the host with the kernel's lane code (split = 1).
+// out: rows*W*3 float64 in image orientation.  counters[8] (optional).
 int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
               double* out, uint64_t* counters) {
     HostScene H;
@@ -200,7 +200,7 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
     return 0;
 }
 
-// BVH shape: out = {n_bnode, bvh_depth, n_qnode, qstack}
+// BVH shape: out[6] = {n_bnode, bvh_depth, n_qnode, qstack, n_bunitc, bvh_obj1}
 int hc_bvh_info(const pt_scene_desc* d, int32_t* out) {
     HostScene H;
     if (!prepare_scene(d, &H).empty()) return -1;
