@@ -183,7 +183,12 @@ struct SceneK {
     double ortho[4];
     double ambient;
     double light_rgb[3];
-    double center[3];
+    double center[3];           // centre of the box of the triangles and the eye: the
+                                // coordinates of unit_eye and of the BVH records
+    double center_s[3];         // centre of the triangles' box: the coordinates of `unit`
+                                // (origins on scene surfaces)
+    const UnitF* unit_eye;      // [n_unit] the uniform units relative to `center`, with
+                                // error bounds valid out to the eye (primary rays)
     const BNode* bnode;         // [n_bnode] BVH of the mesh objects' units (none: n_bnode = 0)
     const UnitF* bunit;         // [n_bunit] those units in leaf order
     int32_t n_bnode, n_bunit, bvh_min_tri, bvh_min_obj;   // lowest triangle / object in it
@@ -205,9 +210,36 @@ struct SceneK {
 // (pixel, sample, bounce, slot>>2); see tests/golden/philox_ref.py.
 // The 4 blocks of one (pixel, sample, bounce) — slots 0..15 — in lockstep:
 // four independent 10-round chains interleaved, instead of one chain at a time
+// Values a caller keeps across its bounce loop, made opaque to the optimiser
+// here (the seed is the same for every lane of a launch): the Philox round-0 products of the pixel and the key schedule are
+// then recomputed per call (a few integer ops) instead of being hoisted out
+// of the loop into registers it does not have (they went to scratch).
+PT_HD uint32_t pt_opaque(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(v));
+#endif
+    return v;
+}
+PT_HD uint32_t pt_opaque_s(uint32_t v) {   // a wave-uniform value (kept in an SGPR)
+#if defined(__HIP_DEVICE_COMPILE__)
+    v = __builtin_amdgcn_readfirstlane(v);
+    asm volatile("" : "+s"(v));
+#endif
+    return v;
+}
+#ifndef PT_RNG_OPQ
+#define PT_RNG_OPQ 0
+#endif
 PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce,
                        uint32_t w[16]) {
+#if PT_RNG_OPQ & 1
+    pixel = pt_opaque(pixel);
+#endif
+#if PT_RNG_OPQ & 2
+    uint32_t k0 = pt_opaque_s((uint32_t)seed), k1 = pt_opaque_s((uint32_t)(seed >> 32));
+#else
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#endif
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
         w[4 * b] = pixel; w[4 * b + 1] = sample; w[4 * b + 2] = bounce; w[4 * b + 3] = (uint32_t)b;

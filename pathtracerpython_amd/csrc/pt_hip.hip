@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __
         J.rr_depth = R.rr_depth;
         D3 P0 = d3(0, 0, 0);
         int tri0 = -1;
-        if (ns > 0 && R.bounces > 0) tri0 = closest<FORCE64, false, BVH>(S, eye, d0, -1, sp, &P0, &cnt);
+        if (ns > 0 && R.bounces > 0) tri0 = closest<FORCE64, false, BVH>(S, eye, d0, -1, sp, &P0, &cnt, true);
         acc = render_lane<FORCE64, COUNT, BVH>(S, J, d0, tri0, P0, sp, &cnt);
     }
     SlotJob j;
@@ -418,19 +418,27 @@ __global__ __launch_bounds__(256) void k_wf_final(SceneK S, RenderK R, const WfP
     store_pixel(R, j, acc, out, R.split);
 }
 
+// the origins the filter's bounds cover: within the surface frame's box
+// (xs), within the box with the eye (xa); outside both -> forced f64
+__device__ __forceinline__ bool in_box(F3 o, float x) {
+    return fabsf(o.x) <= x && fabsf(o.y) <= x && fabsf(o.z) <= x;
+}
+
 __global__ __launch_bounds__(256) void k_intersect(SceneK S, const double* __restrict__ rays,
-                                                   int64_t n, float xb, int32_t* __restrict__ out_tri,
+                                                   int64_t n, float xs, float xa,
+                                                   int32_t* __restrict__ out_tri,
                                                    double* __restrict__ out_p) {
     __shared__ double spill[kSpillSlots][256];
     const Spill sp{&spill[0][threadIdx.x], 256};
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const D3 o = ld3(rays + 6 * i), d = ld3(rays + 6 * i + 3);
-    const F3 oc = to_f3(o - ld3(S.center));
-    const bool in_box = fabsf(oc.x) <= xb && fabsf(oc.y) <= xb && fabsf(oc.z) <= xb;
+    const bool in_s = in_box(to_f3(o - ld3(S.center_s)), xs);
+    const bool in_a = in_box(to_f3(o - ld3(S.center)), xa);
     D3 P = d3(0, 0, 0);
     Counters c;
-    const int t = in_box ? closest<false, false>(S, o, d, -1, sp, &P, &c) : closest<true, false>(S, o, d, -1, sp, &P, &c);
+    const int t = (in_s || in_a) ? closest<false, false>(S, o, d, -1, sp, &P, &c, !in_s)
+                                 : closest<true, false>(S, o, d, -1, sp, &P, &c, true);
     out_tri[i] = t;
     out_p[3 * i] = P.x; out_p[3 * i + 1] = P.y; out_p[3 * i + 2] = P.z;
 }
@@ -438,8 +446,8 @@ __global__ __launch_bounds__(256) void k_intersect(SceneK S, const double* __res
 __global__ __launch_bounds__(256) void k_color(SceneK S, const int32_t* __restrict__ obj,
                                                const double* __restrict__ point,
                                                const double* __restrict__ normal,
-                                               const double* __restrict__ u, int64_t n, float xb,
-                                               double* __restrict__ out) {
+                                               const double* __restrict__ u, int64_t n, float xs,
+                                               float xa, double* __restrict__ out) {
     __shared__ double spill[kSpillSlots][256];
     const Spill sp{&spill[0][threadIdx.x], 256};
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -447,10 +455,11 @@ __global__ __launch_bounds__(256) void k_color(SceneK S, const int32_t* __restri
     const D3 P = ld3(point + 3 * i);
     double uu[12];
     for (int j = 0; j < 12; ++j) uu[j] = u[12 * i + j];
-    const F3 oc = to_f3(P - ld3(S.center));
-    const bool in_box = fabsf(oc.x) <= xb && fabsf(oc.y) <= xb && fabsf(oc.z) <= xb;
+    // nee() tests the uniform units in the surface frame and the BVH in the
+    // frame with the eye: the filter needs the point inside both boxes
+    const bool ok = in_box(to_f3(P - ld3(S.center_s)), xs) && in_box(to_f3(P - ld3(S.center)), xa);
     Counters c;
-    const D3 col = in_box ? nee<false, false>(S, P, ld3(normal + 3 * i), obj[i], -1, uu, sp, &c)
+    const D3 col = ok ? nee<false, false>(S, P, ld3(normal + 3 * i), obj[i], -1, uu, sp, &c)
                           : nee<true, false>(S, P, ld3(normal + 3 * i), obj[i], -1, uu, sp, &c);
     out[3 * i] = col.x; out[3 * i + 1] = col.y; out[3 * i + 2] = col.z;
 }
@@ -461,7 +470,7 @@ struct pt_scene {
     int n_cu = 256;   // compute units of the device (MI355X: 256 in 8 XCDs)
     HostScene host;
     SceneK dev{};
-    float xbound = 0.f;
+    float xb_surf = 0.f, xb_all = 0.f;   // origin boxes of the two filter frames
     void* blob = nullptr;          // all scene tables, one allocation
     StatsDev* stats = nullptr;
     void* out_dev = nullptr;       // pt_render's staging buffer
@@ -493,17 +502,20 @@ struct DeviceGuard {
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
-float box_bound(const HostScene& H) {
-    // origins handed to the filter must lie in the box its constants assume;
-    // recompute X exactly as prepare_scene does (centre / half extent)
+// Origins handed to the filter must lie in the box its bounds assume: the
+// largest centred coordinate of the triangles (surface frame), or of the
+// triangles and the eye (frame with the eye), as prepare_scene's X.
+float box_bound(const HostScene& H, bool with_eye) {
     double X = 0.0;
     const SceneK& K = H.k;
+    const double* c = with_eye ? K.center : K.center_s;
     for (const TriD& T : H.trid) {
         const double* vs[3] = {T.v1, T.v2, T.v3};
         for (int v = 0; v < 3; ++v)
-            for (int i = 0; i < 3; ++i) X = std::max(X, fabs(vs[v][i] - K.center[i]));
+            for (int i = 0; i < 3; ++i) X = std::max(X, fabs(vs[v][i] - c[i]));
     }
-    for (int i = 0; i < 3; ++i) X = std::max(X, fabs(K.eye[i] - K.center[i]));
+    if (with_eye)
+        for (int i = 0; i < 3; ++i) X = std::max(X, fabs(K.eye[i] - c[i]));
     return (float)X;
 }
 }  // namespace
@@ -582,7 +594,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         if (prop.multiProcessorCount > 0) s->n_cu = prop.multiProcessorCount;
     }
     HostScene& H = s->host;
-    constexpr int kArrays = 13;
+    constexpr int kArrays = 14;
     const size_t sz[kArrays] = {H.unit.size() * sizeof(UnitF), H.trid.size() * sizeof(TriD),
                                 H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
                                 H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
@@ -590,11 +602,11 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
                                 H.tri_grp.size() * sizeof(int32_t),
                                 H.bnode.size() * sizeof(BNode), H.bunit.size() * sizeof(UnitF),
                                 H.cnode.size() * sizeof(CNode), H.qnode.size() * sizeof(QNode),
-                                H.bunitc.size() * sizeof(UnitC)};
+                                H.bunitc.size() * sizeof(UnitC), H.unit_eye.size() * sizeof(UnitF)};
     const void* src[kArrays] = {H.unit.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
                                 H.mat.data(), H.light_tri.data(), H.light_cum.data(),
                                 H.tri_grp.data(), H.bnode.data(), H.bunit.data(), H.cnode.data(),
-                                H.qnode.data(), H.bunitc.data()};
+                                H.qnode.data(), H.bunitc.data(), H.unit_eye.data()};
     size_t off[kArrays], total = 0;
     for (int i = 0; i < kArrays; ++i) { off[i] = total; total += align_up(sz[i]); }
     int rc = PT_OK;
@@ -622,7 +634,9 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     s->dev.cnode = (const CNode*)(b + off[10]);
     s->dev.qnode = (const QNode*)(b + off[11]);
     s->dev.bunitc = H.bunitc.empty() ? nullptr : (const UnitC*)(b + off[12]);
-    s->xbound = box_bound(H);
+    s->dev.unit_eye = (const UnitF*)(b + off[13]);
+    s->xb_surf = box_bound(H, false);
+    s->xb_all = box_bound(H, true);
     *out = s;
     return rc;
 }
@@ -1135,7 +1149,7 @@ int pt_intersect_objects(pt_scene* s, const double* rays, int64_t n, int32_t* ou
     if (!rc) rc = dev_alloc_copy(&d_tri, (const int32_t*)nullptr, (size_t)n);
     if (!rc) {
         hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s->stream,
-                           s->dev, d_rays, n, s->xbound, d_tri, d_p);
+                           s->dev, d_rays, n, s->xb_surf, s->xb_all, d_tri, d_p);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
         if (e == hipSuccess) e = hipMemcpy(out_tri, d_tri, n * sizeof(int32_t), hipMemcpyDeviceToHost);
@@ -1165,7 +1179,7 @@ int pt_compute_color(pt_scene* s, const int32_t* obj, const double* point, const
     if (!rc) rc = dev_alloc_copy(&d_out, (const double*)nullptr, (size_t)n * 3);
     if (!rc) {
         hipLaunchKernelGGL(k_color, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s->stream,
-                           s->dev, d_obj, d_pt, d_n, d_u, n, s->xbound, d_out);
+                           s->dev, d_obj, d_pt, d_n, d_u, n, s->xb_surf, s->xb_all, d_out);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
         if (e == hipSuccess) e = hipMemcpy(out_rgb, d_out, n * 3 * sizeof(double), hipMemcpyDeviceToHost);

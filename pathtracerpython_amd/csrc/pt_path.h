@@ -955,18 +955,23 @@ PT_HD void ctrav_qnode(ClosestTrav& T, const ClosestStack& K, const SceneK& S, c
 // not be normalised (utils.py:110).  ogrp: coplanar group of the triangle the
 // origin lies on (-1: none).
 // BVH = false: the instantiation for scenes without meshes (no BVH code)
+// eye: o may lie anywhere in the box of the triangles and the eye (primary
+// rays: the unit_eye records), else on a scene surface (the `unit` records).
 template <bool FORCE64, bool COUNT, bool BVH = true>
-PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, const Spill& sp, D3* P, Counters* cnt) {
+PT_HD int closest(const SceneK& S, D3 o, D3 d, int ogrp, const Spill& sp, D3* P, Counters* cnt,
+                  bool eye) {
     const D3 dn = unit(d);
     ClosestAcc acc = closest_init();
     if (!FORCE64) {
         sp.put3(kSpP, o);
         sp.put3(kSpNd, d);
         const F3 o32 = to_f3(o - ld3(S.center));
+        const F3 o32u = eye ? o32 : to_f3(o - ld3(S.center_s));
+        const UnitF* units = eye ? S.unit_eye : S.unit;
         const F3 d32 = to_f3(dn);
         for (int u = 0; u < S.n_unit; ++u) {
-            const UnitF U = S.unit[u];
-            closest_unit<COUNT>(S, U, origin_u(U, o32), d32, U.grp == ogrp, sp, kSpP, kSpNd,
+            const UnitF U = units[u];
+            closest_unit<COUNT>(S, U, origin_u(U, o32u), d32, U.grp == ogrp, sp, kSpP, kSpNd,
                                 &acc, cnt);
         }
         if (BVH && S.n_bnode) {   // the meshes: closest ray only
@@ -988,11 +993,11 @@ PT_HD D3 nee(const SceneK& S, D3 P, D3 n, int obj, int ogrp, const double u[12],
     ShadowSet sh;
     sp.put3(kSpP, P);
     shadow_setup<COUNT>(S, P, n, u, &sh, sp);
-    const F3 o32 = to_f3(P - ld3(S.center));
+    const F3 o32 = to_f3(P - ld3(S.center)), o32u = to_f3(P - ld3(S.center_s));
     for (int u = 0; u < S.n_obj_unit; ++u) {
         if (PT_WAVE_ALL(sh.occ[0] && sh.occ[1] && sh.occ[2])) break;
         const UnitF U = S.unit[u];
-        const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
+        const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32u);
         fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, true, false, &sh, F3{0.f, 0.f, 0.f},
                                    nullptr, sp, cnt);
     }
@@ -1116,7 +1121,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         }
         // one pass: 3 shadow rays + the next ray's closest hit, same origin
         sp.put3(kSpNd, nd);
-        const F3 o32 = to_f3(P - ld3(S.center));
+        const F3 o32u = to_f3(P - ld3(S.center_s));   // the uniform units' frame
         const F3 n32 = to_f3(unit(nd));
         ClosestAcc ca = closest_init();
         const bool any_trace = PT_WAVE_ANY(trace);
@@ -1124,7 +1129,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
             float oc[kLightSamples] = {-1.0f, -1.0f, -1.0f};
             for (int u = 0; u < S.n_obj_unit; ++u) {
                 const UnitF U = S.unit[u];
-                const OriginU O = origin_u(U, o32);
+                const OriginU O = origin_u(U, o32u);
                 const bool do_shadow =
                     PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));
                 fused_unit<FORCE64, COUNT, true>(S, U, O, U.grp == ogrp, do_shadow, any_trace,
@@ -1135,13 +1140,14 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         } else {
             for (int u = 0; u < S.n_obj_unit; ++u) {
                 const UnitF U = S.unit[u];
-                const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32);
+                const OriginU O = FORCE64 ? OriginU{0.f, 0.f, 0.f, 0.f, 0.f} : origin_u(U, o32u);
                 const bool do_shadow = PT_WAVE_ANY(!(sh.occ[0] && sh.occ[1] && sh.occ[2]));
                 fused_unit<FORCE64, COUNT>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
                                            &ca, sp, cnt);
             }
         }
         if (BVH && S.n_bnode) {   // the meshes: shadows as a packet, the closest ray ordered
+            const F3 o32 = to_f3(P - ld3(S.center));   // the BVH's frame
             const bool ordered = !FORCE64 && S.bvh_depth < kBvhStack;
             if (ordered) {
 #ifndef PT_ABL_NOBVHSHADOW
@@ -1156,7 +1162,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         if (!FORCE64 && any_trace) {
             for (int u = S.n_obj_unit; u < S.n_unit; ++u) {   // the light's units
                 const UnitF U = S.unit[u];
-                closest_unit<COUNT>(S, U, origin_u(U, o32), n32, U.grp == ogrp, sp, kSpP, kSpNd,
+                closest_unit<COUNT>(S, U, origin_u(U, o32u), n32, U.grp == ogrp, sp, kSpP, kSpNd,
                                     &ca, cnt);
             }
         }

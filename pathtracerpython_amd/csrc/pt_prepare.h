@@ -18,6 +18,7 @@ namespace pt {
 
 struct HostScene {
     std::vector<UnitF> unit;
+    std::vector<UnitF> unit_eye;
     std::vector<UnitF> bunit;
     std::vector<UnitC> bunitc;   // bunit in 64-B form (empty: not representable)
     std::vector<BNode> bnode;
@@ -396,9 +397,16 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         if (t < d->n_obj_tri ? (o < 0 || o >= d->n_obj) : (o != d->n_obj))
             return "tri_obj out of range (objects first, then light = n_obj)";
     }
-    // scene box (vertices and eye) -> centre and half extent X
+    // Two coordinate frames for the f32 filter, each a box centre and half
+    // extent X bounding every origin expressed in it:
+    //   "all" (C, X): the triangles and the eye — primary rays start at the
+    //       eye; the BVH records and unit_eye use it;
+    //   "surface" (Cs, Xs): the triangles alone — every later ray starts on a
+    //       scene surface; the uniform units (`unit`) use it, so their error
+    //       bounds, which grow with X, are not inflated by the eye's distance
+    //       (Cornell: Xs = 8.1 vs X = 19.2).
     double lo[3], hi[3];
-    for (int i = 0; i < 3; ++i) lo[i] = hi[i] = d->eye[i];
+    for (int i = 0; i < 3; ++i) lo[i] = INFINITY, hi[i] = -INFINITY;
     for (int t = 0; t < T; ++t)
         for (int v = 0; v < 3; ++v)
             for (int i = 0; i < 3; ++i) {
@@ -407,6 +415,18 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
                 lo[i] = std::min(lo[i], x);
                 hi[i] = std::max(hi[i], x);
             }
+    for (int i = 0; i < 3; ++i)
+        if (!isfinite(d->eye[i])) return "non-finite eye";
+    double Cs[3], Xs = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        Cs[i] = 0.5 * (lo[i] + hi[i]);
+        Xs = std::max(Xs, 0.5 * (hi[i] - lo[i]));
+    }
+    Xs = Xs * 1.001 + 1e-6;
+    for (int i = 0; i < 3; ++i) {
+        lo[i] = std::min(lo[i], d->eye[i]);
+        hi[i] = std::max(hi[i], d->eye[i]);
+    }
     double C[3], X = 0.0;
     for (int i = 0; i < 3; ++i) {
         C[i] = 0.5 * (lo[i] + hi[i]);
@@ -424,8 +444,26 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     std::vector<TriB> tb(T);
     struct TriE { float eo, ed, g; };   // barycentric bound coefficients
     std::vector<TriE> te(T);
-    const D3 Cd = d3(C[0], C[1], C[2]);
+    std::vector<PlaneD> pls(T);          // the same in the surface frame
+    std::vector<TriB> tbs(T);
+    std::vector<TriE> tes(T);
+    const D3 Cd = d3(C[0], C[1], C[2]), Cds = d3(Cs[0], Cs[1], Cs[2]);
     auto l1 = [](double a, double b, double c) { return fabs(a) + fabs(b) + fabs(c); };
+    // bound on |aff3(f32(G), f32(C), f32(x)) - (G.x + C)| for |x_i| <= Xb (see below)
+    auto aff_err = [u](const double G[3], double Cc, double Xb) {
+        double e = fabs((double)(float)Cc - Cc), g1 = 0.0;
+        int k = 0;
+        for (int i = 0; i < 3; ++i) {
+            const double g = (double)(float)G[i];
+            e += fabs(g - G[i]) * Xb;
+            if (g != 0.0) {
+                e += u * fabs(g) * Xb;
+                ++k;
+            }
+            g1 += fabs(g);
+        }
+        return e + k * u * (g1 * Xb + fabs((double)(float)Cc)) * (1 + 4 * u) + 1e-30;
+    };
     const double s = 1.25;   // safety factor over the first-order bounds below
     for (int t = 0; t < T; ++t) {
         const D3 v1 = tri_vertex(d, t, 0), v2 = tri_vertex(d, t, 1), v3 = tri_vertex(d, t, 2);
@@ -444,38 +482,56 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         memcpy(R.n, d->tri_n + 3 * t, 3 * sizeof(double));
         rotation_for_normal(R.n, &R);
 
-        // f32 filter data in centred coordinates
-        const D3 w1 = v1 - Cd, w2 = v2 - Cd, w3 = v3 - Cd;
-        const D3 e1 = w2 - w1, e2 = w3 - w1, N = cross(e1, e2);
-        const double NN = dot(N, N);
-        PlaneD& P = pl[t];
-        TriB& B = tb[t];
-        B = TriB{};
-        TriE& BE = te[t];
-        BE = TriE{};
-        P.ok = (cn > 0.0) && (NN > 0.0) && isfinite(cn);
-        if (!P.ok) continue;   // degenerate: the reference's NaN normal never hits
-        const D3 gb = cross(e2, N) * (1.0 / NN), gc = cross(N, e1) * (1.0 / NN);
-        const double cb = -dot(gb, w1), cc = -dot(gc, w1);
-        const double chn = -(E.vp[0] * w1.x + E.vp[1] * w1.y + E.vp[2] * w1.z);
-        for (int i = 0; i < 3; ++i) P.n[i] = E.vp[i];
-        P.cn = chn;
-        B.gb[0] = (float)gb.x; B.gb[1] = (float)gb.y; B.gb[2] = (float)gb.z; B.cb = (float)cb;
-        B.gc[0] = (float)gc.x; B.gc[1] = (float)gc.y; B.gc[2] = (float)gc.z; B.cc = (float)cc;
-        // An f32 affine form g.x + c at |x_i| <= X, evaluated as an fma chain
-        // from rounded inputs, errs by <= 5u(|g|_1 X + |c|) (input and
-        // coefficient rounding 2u|g|_1 X + u|c|, three fmas 3u(...)); we take
-        // 8u, times the safety factor s.  Direction forms: |d_i| <= 1.
-        const double n1 = l1((float)P.n[0], (float)P.n[1], (float)P.n[2]) * (1 + 4 * u);
-        const double gb1 = l1(B.gb[0], B.gb[1], B.gb[2]) * (1 + 4 * u);
-        const double gc1 = l1(B.gc[0], B.gc[1], B.gc[2]) * (1 + 4 * u);
-        P.eh = s * 8 * u * (n1 * X + fabs(chn));
-        // q's own error, plus 8u n1 >= 8u|q| covering the rounding of 1/q and t
-        P.eq = s * 8 * u * n1 + 8 * u * n1;
-        // x2: one bound for beta, gamma (error <= del/2) and alpha (<= del)
-        BE.eo = f32_up(2 * (s * 8 * u * std::max(gb1 * X + fabs(cb), gc1 * X + fabs(cc)) + 8 * u));
-        BE.ed = f32_up(2 * s * 8 * u * std::max(gb1, gc1));
-        BE.g = f32_up(2 * std::max(gb1, gc1) * (1 + 1e-3));
+        // f32 filter data in centred coordinates, once per frame (f = 0: "all",
+        // f = 1: "surface"); only the constants and the X-dependent bounds
+        // differ between the frames
+        for (int f = 0; f < 2; ++f) {
+            const D3 Cf = f ? Cds : Cd;
+            const double Xf = f ? Xs : X;
+            const D3 w1 = v1 - Cf, w2 = v2 - Cf, w3 = v3 - Cf;
+            const D3 e1 = w2 - w1, e2 = w3 - w1, N = cross(e1, e2);
+            const double NN = dot(N, N);
+            PlaneD& P = f ? pls[t] : pl[t];
+            TriB& B = f ? tbs[t] : tb[t];
+            B = TriB{};
+            TriE& BE = f ? tes[t] : te[t];
+            BE = TriE{};
+            P.ok = (cn > 0.0) && (NN > 0.0) && isfinite(cn);
+            if (!P.ok) continue;   // degenerate: the reference's NaN normal never hits
+            const D3 gb = cross(e2, N) * (1.0 / NN), gc = cross(N, e1) * (1.0 / NN);
+            const double cb = -dot(gb, w1), cc = -dot(gc, w1);
+            const double chn = -(E.vp[0] * w1.x + E.vp[1] * w1.y + E.vp[2] * w1.z);
+            for (int i = 0; i < 3; ++i) P.n[i] = E.vp[i];
+            P.cn = chn;
+            B.gb[0] = (float)gb.x; B.gb[1] = (float)gb.y; B.gb[2] = (float)gb.z; B.cb = (float)cb;
+            B.gc[0] = (float)gc.x; B.gc[1] = (float)gc.y; B.gc[2] = (float)gc.z; B.cc = (float)cc;
+            // Error bounds of the kernel's f32 forms (aff3 / lin3, pt_core.h):
+            // an affine form g.x + c at |x_i| <= X with g = f32(G), c = f32(C),
+            // x = f32(x_exact), evaluated as aff3's fma chain, errs by at most
+            //   sum_i |g_i - G_i| X + |c - C|           (coefficient rounding, exact)
+            // + u sum_i |g_i| X                        (input rounding)
+            // + k u (|g|_1 X + |c|)                    (one rounding per fma
+            //   whose product is nonzero: an fma with g_i = 0 returns its addend
+            //   exactly), k = nonzero coefficients;
+            // a direction form g.d (|d_i| <= 1, lin3) likewise with X = 1, c = 0.
+            // For a general plane this is <= 5u(|g|_1 X + |c|); for an
+            // axis-aligned one (walls: g one-hot and exact) ~2u(X + |c|), which
+            // decides most tests of lines grazing their edges in f32.  The
+            // safety factor s covers second-order terms and the reference's own
+            // f64 rounding (~1e-16 relative).
+            const double nd3[3] = {E.vp[0], E.vp[1], E.vp[2]};
+            const double gbd[3] = {gb.x, gb.y, gb.z}, gcd[3] = {gc.x, gc.y, gc.z};
+            const double n1 = l1((float)P.n[0], (float)P.n[1], (float)P.n[2]) * (1 + 4 * u);
+            const double gb1 = l1(B.gb[0], B.gb[1], B.gb[2]) * (1 + 4 * u);
+            const double gc1 = l1(B.gc[0], B.gc[1], B.gc[2]) * (1 + 4 * u);
+            P.eh = s * aff_err(nd3, chn, Xf);
+            // q's own error, plus 8u n1 >= 8u|q| covering the rounding of 1/q and t
+            P.eq = s * aff_err(nd3, 0.0, 1.0) + 8 * u * n1;
+            // x2: one bound for beta, gamma (error <= del/2) and alpha (<= del)
+            BE.eo = f32_up(2 * (s * std::max(aff_err(gbd, cb, Xf), aff_err(gcd, cc, Xf)) + 8 * u));
+            BE.ed = f32_up(2 * s * std::max(aff_err(gbd, 0.0, 1.0), aff_err(gcd, 0.0, 1.0)));
+            BE.g = f32_up(2 * std::max(gb1, gc1) * (1 + 1e-3));
+        }
     }
     // coplanar groups: triangle t joins the group of an earlier
     // representative r when every vertex of t lies within 1e-12 of r's plane
@@ -532,48 +588,61 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     for (int t = 0; t < d->n_obj_tri; ++t) obj_ntri[d->tri_obj[t]]++;
     auto in_bvh = [&](int t) { return t < d->n_obj_tri && obj_ntri[d->tri_obj[t]] >= kBvhMinTris; };
     H->unit.clear();
+    H->unit_eye.clear();
     H->bunit.clear();
+    // one unit record in frame f (0: all, 1: surface) for triangles t (, t + 1)
+    auto make_unit = [&](int t, bool pair, int f) {
+        const std::vector<PlaneD>& PL = f ? pls : pl;
+        const std::vector<TriB>& TB = f ? tbs : tb;
+        const std::vector<TriE>& TE = f ? tes : te;
+        UnitF U{};
+        const PlaneD& P = PL[t];
+        U.count = pair ? 2 : 1;
+        U.grp = H->tri_grp[t];
+        U.obj = d->tri_obj[t];
+        U.tri[0] = TB[t];
+        U.tri[1] = pair ? TB[t + 1] : TriB{};
+        U.t[0] = t;
+        U.t[1] = pair ? t + 1 : t;
+        U.eo = TE[t].eo;
+        U.ed = TE[t].ed;
+        U.g = TE[t].g;
+        if (!P.ok) {   // degenerate: dt = -inf -> certain miss, never a candidate
+            U.eh = -INFINITY;
+            U.eq = 0.f;
+            U.qhi = INFINITY;
+        } else {
+            double eh = P.eh, eq = P.eq;
+            if (pair) {
+                eh = std::max(eh, PL[t + 1].eh) + 1e-9;
+                eq = std::max(eq, PL[t + 1].eq) + 1e-9;
+                // one bound for both members (the kernel evaluates del once per
+                // ray and unit)
+                U.eo = f32_up(std::max(TE[t].eo, TE[t + 1].eo) + 2e-9);
+                U.ed = std::max(TE[t].ed, TE[t + 1].ed);
+                U.g = std::max(TE[t].g, TE[t + 1].g);
+            }
+            for (int i = 0; i < 3; ++i) U.n[i] = (float)P.n[i];
+            U.cn = (float)P.cn;
+            U.eh = f32_up(eh);
+            U.eq = f32_up(eq);
+            U.qhi = f32_up((1e-5 + eq) * (1 + 1e-4));
+        }
+        return U;
+    };
     for (int part = 0; part < 2; ++part) {
         const int t_begin = part == 0 ? 0 : d->n_obj_tri, t_end = part == 0 ? d->n_obj_tri : T;
         for (int t = t_begin; t < t_end;) {
-            UnitF U{};
-            const PlaneD& P = pl[t];
-            const bool pair = (t + 1 < t_end) && P.ok && pl[t + 1].ok &&
+            const bool pair = (t + 1 < t_end) && pl[t].ok && pl[t + 1].ok &&
                               H->tri_grp[t] >= 0 && H->tri_grp[t + 1] == H->tri_grp[t] &&
                               d->tri_obj[t + 1] == d->tri_obj[t];
-            U.count = pair ? 2 : 1;
-            U.grp = H->tri_grp[t];
-            U.obj = d->tri_obj[t];
-            U.tri[0] = tb[t];
-            U.tri[1] = pair ? tb[t + 1] : TriB{};
-            U.t[0] = t;
-            U.t[1] = pair ? t + 1 : t;
-            U.eo = te[t].eo;
-            U.ed = te[t].ed;
-            U.g = te[t].g;
-            if (!P.ok) {   // degenerate: dt = -inf -> certain miss, never a candidate
-                U.eh = -INFINITY;
-                U.eq = 0.f;
-                U.qhi = INFINITY;
+            if (in_bvh(t)) {
+                H->bunit.push_back(make_unit(t, pair, 0));
             } else {
-                double eh = P.eh, eq = P.eq;
-                if (pair) {
-                    eh = std::max(eh, pl[t + 1].eh) + 1e-9;
-                    eq = std::max(eq, pl[t + 1].eq) + 1e-9;
-                    // one bound for both members (the kernel evaluates del once per
-                    // ray and unit)
-                    U.eo = f32_up(std::max(te[t].eo, te[t + 1].eo) + 2e-9);
-                    U.ed = std::max(te[t].ed, te[t + 1].ed);
-                    U.g = std::max(te[t].g, te[t + 1].g);
-                }
-                for (int i = 0; i < 3; ++i) U.n[i] = (float)P.n[i];
-                U.cn = (float)P.cn;
-                U.eh = f32_up(eh);
-                U.eq = f32_up(eq);
-                U.qhi = f32_up((1e-5 + eq) * (1 + 1e-4));
+                H->unit.push_back(make_unit(t, pair, 1));
+                H->unit_eye.push_back(make_unit(t, pair, 0));
             }
-            (in_bvh(t) ? H->bunit : H->unit).push_back(U);
-            t += U.count;
+            t += pair ? 2 : 1;
         }
         if (part == 0) H->k.n_obj_unit = (int32_t)H->unit.size();
     }
@@ -608,6 +677,7 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         K.eye[i] = d->eye[i];
         K.light_rgb[i] = d->light_rgb[i];
         K.center[i] = C[i];
+        K.center_s[i] = Cs[i];
     }
     for (int i = 0; i < 4; ++i) K.ortho[i] = d->ortho[i];
     K.ambient = d->ambient;
@@ -622,6 +692,7 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
 // host pointers (for the host-side check build)
 inline void bind_host(HostScene* H) {
     H->k.unit = H->unit.data();
+    H->k.unit_eye = H->unit_eye.data();
     H->k.bnode = H->bnode.data();
     H->k.cnode = H->cnode.data();
     H->k.qnode = H->qnode.data();

@@ -125,8 +125,8 @@ PT_HD uint32_t wf_start(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfC
     const F3 o32 = to_f3(eye - ld3(S.center));
     const F3 d32 = to_f3(dn);
     ClosestAcc acc = closest_init();
-    for (int u = 0; u < S.n_unit; ++u) {
-        const UnitF U = S.unit[u];
+    for (int u = 0; u < S.n_unit; ++u) {   // from the eye: the unit_eye records
+        const UnitF U = S.unit_eye[u];
         closest_unit<false>(S, U, origin_u(U, o32), d32, U.grp == -1, sp, kSpP, kSpNd, &acc,
                             nullptr);
     }
@@ -168,7 +168,8 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
         else kk = kn / q;
     }
     sp.put3(kSpNd, nd);
-    const F3 o32 = to_f3(P - ld3(S.center));
+    const F3 o32 = to_f3(P - ld3(S.center));      // the BVH's frame (the walks)
+    const F3 o32u = to_f3(P - ld3(S.center_s));   // the uniform units' frame
     const F3 n32 = to_f3(unit(nd));
     ClosestAcc ca = closest_init();
     const bool any_trace = PT_WAVE_ANY(trace);
@@ -176,7 +177,7 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
         float oc[kLightSamples] = {-1.0f, -1.0f, -1.0f};
         for (int u = 0; u < S.n_obj_unit; ++u) {
             const UnitF U = S.unit[u];
-            const OriginU O = origin_u(U, o32);
+            const OriginU O = origin_u(U, o32u);
             const bool do_shadow = PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));
             fused_unit<false, false, true>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
                                            &ca, sp, nullptr, 15u, oc);
@@ -187,7 +188,7 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
     if (any_trace) {
         for (int u = S.n_obj_unit; u < S.n_unit; ++u) {   // the light's units
             const UnitF U = S.unit[u];
-            closest_unit<false>(S, U, origin_u(U, o32), n32, U.grp == ogrp, sp, kSpP, kSpNd, &ca,
+            closest_unit<false>(S, U, origin_u(U, o32u), n32, U.grp == ogrp, sp, kSpP, kSpNd, &ca,
                                 nullptr);
         }
     }

@@ -68,11 +68,11 @@ int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
             // counters requested: the count-mode lane code (exact first
             // occluders); else the render kernel's own (object-level) one
             if (force64) {
-                if (p->bounces > 0) tri0 = closest<true, false>(H.k, eye, d0, -1, sp, &P0, &c);
+                if (p->bounces > 0) tri0 = closest<true, false>(H.k, eye, d0, -1, sp, &P0, &c, true);
                 acc = counters ? render_lane<true, true>(H.k, J, d0, tri0, P0, sp, &c)
                                : render_lane<true, false>(H.k, J, d0, tri0, P0, sp, &c);
             } else {
-                if (p->bounces > 0) tri0 = closest<false, false>(H.k, eye, d0, -1, sp, &P0, &c);
+                if (p->bounces > 0) tri0 = closest<false, false>(H.k, eye, d0, -1, sp, &P0, &c, true);
                 acc = counters ? render_lane<false, true>(H.k, J, d0, tri0, P0, sp, &c)
                                : render_lane<false, false>(H.k, J, d0, tri0, P0, sp, &c);
             }
@@ -227,7 +227,7 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
     std::uniform_real_distribution<double> U(0.0, 1.0);
     std::normal_distribution<double> N(0.0, 1.0);
     int64_t wrong = 0, amb = 0, tests = 0, cand = 0, mdiff = 0;
-    const D3 C = ld3(H.k.center);
+    const D3 C = ld3(H.k.center), Cs = ld3(H.k.center_s);
     for (int64_t i = 0; i < n_rays; ++i) {
         D3 o;
         if (i % 4 == 0) {
@@ -242,14 +242,26 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
         if (i % 3 == 0) {   // aim near a random vertex: many near-edge lines
             const TriD& T = H.trid[rng() % H.trid.size()];
             dir = ld3(T.v1) + d3(N(rng), N(rng), N(rng)) * 1e-3 - o;
+        } else if (i % 3 == 1 && (i / 3) % 2 == 0) {
+            // aim at a point of a random edge, off by 1e-2 .. 1e-9: lines
+            // grazing edges (e.g. from the ceiling across a wall's top edge)
+            const TriD& T = H.trid[rng() % H.trid.size()];
+            const D3 vv[3] = {ld3(T.v1), ld3(T.v2), ld3(T.v3)};
+            const int e = (int)(rng() % 3);
+            const double a = U(rng), sc = pow(10.0, -2.0 - 7.0 * U(rng));
+            dir = vv[e] + (vv[(e + 1) % 3] - vv[e]) * a + d3(N(rng), N(rng), N(rng)) * sc - o;
         }
         const D3 dn = unit(dir);
-        const F3 o32 = to_f3(o - C), d32 = to_f3(dn);
+        const bool at_eye = i % 4 == 0;
+        // frames: the eye's origins test unit_eye, surface origins `unit`
+        // (surface frame); the BVH units are in the frame with the eye
+        const F3 o32 = to_f3(o - C), o32s = to_f3(o - Cs), d32 = to_f3(dn);
         const double lim = 0.5 + 40.0 * U(rng);   // a shadow range
         const float hlo = (float)(sqrt(lim) * (1 - 1e-6)), hhi = (float)(sqrt(lim) * (1 + 1e-6));
         for (int u = 0; u < H.k.n_unit + H.k.n_bunit; ++u) {   // uniform and BVH units
-            const UnitF& U = u < H.k.n_unit ? H.unit[u] : H.bunit[u - H.k.n_unit];
-            const OriginU O = origin_u(U, o32);
+            const bool uni = u < H.k.n_unit;
+            const UnitF& U = uni ? (at_eye ? H.unit_eye[u] : H.unit[u]) : H.bunit[u - H.k.n_unit];
+            const OriginU O = origin_u(U, (uni && !at_eye) ? o32s : o32);
             const RayPlane pc = ray_plane(U, O.h, d32, INFINITY, INFINITY);
             const RayPlane ps = ray_plane(U, O.h, d32, hlo, hhi);
             for (int i = 0; i < U.count; ++i) {
