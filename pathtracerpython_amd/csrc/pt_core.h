@@ -232,6 +232,14 @@ PT_HD uint32_t pt_opaque_s(uint32_t v) {   // a wave-uniform value (kept in an S
 #endif
 PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce,
                        uint32_t w[16]) {
+#ifdef PT_ABL_CHEAPRNG   // timing ablation only (a different stream)
+    uint32_t h = pixel * 0x9E3779B1u ^ sample * 0x85EBCA77u ^ bounce * 0xC2B2AE3Du ^ (uint32_t)seed;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h += 0x297A2D39u; w[i] = h;
+    }
+    return;
+#endif
 #if PT_RNG_OPQ & 1
     pixel = pt_opaque(pixel);
 #endif

@@ -134,7 +134,10 @@ template <bool FORCE64, bool COUNT, bool BVH>
 // 4 waves/SIMD (<= 128 VGPRs, a little scratch spill outside the triangle
 // loops): 9.5 ms vs 10.8 ms at 3 waves and 15.3 ms at 2 on the 512^2 x 64spp
 // bench (MI355X), see DESIGN.md §5.
-__global__ __launch_bounds__(256, 4) void k_render(SceneK S, RenderK R, void* __restrict__ out,
+#ifndef PT_RENDER_WAVES
+#define PT_RENDER_WAVES 4
+#endif
+__global__ __launch_bounds__(256, PT_RENDER_WAVES) void k_render(SceneK S, RenderK R, void* __restrict__ out,
                                                 StatsDev* __restrict__ st) {
     __shared__ double spill[kSpillSlots][256];
     const Spill sp{&spill[0][threadIdx.x], 256};
@@ -201,14 +204,34 @@ __device__ __forceinline__ void wf_append(bool want, int32_t* counter, int32_t* 
     base = __shfl(base, (int)leader);
     if (want) list[base + (int32_t)lanes_below(m)] = v;
 }
-// wave-aggregated fetch of the next list positions for the lanes that need one
-__device__ __forceinline__ int32_t wf_fetch(bool need, int32_t* head) {
+// Next list positions for the lanes that need one.  A wave claims a chunk of
+// kWfChunk consecutive positions with one atomic on the list head and hands
+// them out to its lanes as they need work; it claims the next chunk only when
+// this one runs out (one global atomic per ~kWfChunk queries instead of one
+// per refill turn).  [cb, ce): the wave's unclaimed rest (wave-uniform).
+#ifndef PT_WF_CHUNK
+#define PT_WF_CHUNK 64
+#endif
+constexpr int32_t kWfChunk = PT_WF_CHUNK;
+static_assert(kWfChunk >= 64, "a refill turn can need a position for every lane of a wave");
+__device__ __forceinline__ int32_t wf_fetch(bool need, int32_t* head, int32_t& cb, int32_t& ce) {
     const uint64_t m = __ballot(need);
-    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-    int32_t base = 0;
-    if (lane_id() == leader) base = atomicAdd(head, (int32_t)__popcll(m));
-    base = __shfl(base, (int)leader);
-    return base + (int32_t)lanes_below(m);
+    const int32_t n = (int32_t)__popcll(m);
+    const int32_t idx = (int32_t)lanes_below(m);   // rank among the needing lanes
+    const int32_t avail = ce - cb;
+    int32_t pos = cb + idx;
+    if (n > avail) {   // wave-uniform: claim the next chunk
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+        int32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(head, kWfChunk);
+        base = __shfl(base, (int)leader);
+        if (idx >= avail) pos = base + (idx - avail);
+        cb = base + (n - avail);
+        ce = base + kWfChunk;
+    } else {
+        cb += n;
+    }
+    return pos;
 }
 
 __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t step,
@@ -242,10 +265,23 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
 // for its longest node run, and lanes whose walk ended are refilled every
 // turn.  Every turn makes progress (a node step, a leaf or a fetch), and a
 // lane whose list is exhausted stays idle, so the loop drains.
-#ifndef PT_WALK_WAVES
-#define PT_WALK_WAVES 1
+// Walk stacks: kWalkStack entries per work-item, the first kWalkStackLds in
+// shared memory (the top of a stack, where nearly all pushes and pops land),
+// the rest in global memory.  Smaller shared-memory stacks let more
+// work-groups share a CU (the walks wait on dependent node loads: occupancy
+// is their latency hiding).
+#ifndef PT_SHADOW_WAVES
+#define PT_SHADOW_WAVES 1
 #endif
-constexpr int kWalkStack = 32;   // entries of a walk kernel's shared-memory stack
+#ifndef PT_CLOSEST_WAVES
+#define PT_CLOSEST_WAVES 5
+#endif
+#ifndef PT_WALK_STACK_LDS
+#define PT_WALK_STACK_LDS 16
+#endif
+constexpr int kWalkStack = 32;                   // entries of a walk kernel's stack
+constexpr int kWalkStackLds = PT_WALK_STACK_LDS;  // of them in shared memory
+constexpr int kWalkStackGlobal = kWalkStack - kWalkStackLds;
 // COUNT (PT_FLAG_WALK_COUNT launches only): per-query work of the walk —
 // queries, 4-wide node visits, leaf-unit tests — summed into wc[0..2]
 // (the walks' algorithmic bytes).
@@ -265,18 +301,21 @@ __device__ __forceinline__ void flush_walk_counts(uint32_t q, uint32_t nodes, ui
 __device__ __forceinline__ uint32_t leaf_units(int ref) { return (uint32_t)(~ref) & 7u; }
 
 template <bool UC, bool COUNT>
-__global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPath* __restrict__ W,
+__global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, WfPath* __restrict__ W,
                                                    WfShadowQ* __restrict__ SQ,
                                                    const int32_t* __restrict__ list, int32_t* counters,
-                                                   int32_t thr, unsigned long long* wc) {
+                                                   int32_t thr, unsigned long long* wc,
+                                                   int* __restrict__ ovf) {
     uint32_t c_q = 0, c_nodes = 0, c_units = 0;
     const int32_t count = counters[0];
+    int32_t cb = 0, ce = 0;   // this wave's claimed list positions (wf_fetch)
     int32_t slot = -1;
     bool exhausted = false;
-    // the walk stack in shared memory (this kernel has no other use for it):
-    // kWalkStack x 4 B per lane, 32 KB per block
-    __shared__ int stack[kWalkStack][256];
-    const ShadowStack K{&stack[0][threadIdx.x], 256};
+    // the walk stack: its top kWalkStackLds entries in shared memory
+    // (4 B each per lane), the rest in global memory
+    __shared__ int stack[kWalkStackLds][256];
+    const int lanes = (int)gridDim.x * 256, gl = (int)(blockIdx.x * 256u + threadIdx.x);
+    const ShadowStack K{&stack[0][threadIdx.x], 256, ovf + gl, lanes, kWalkStackLds};
     ShadowSet sh;
     ShadowTrav T;
     T.ref = kNoRef;
@@ -285,7 +324,7 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
-            const int32_t i = wf_fetch(need, &counters[1]);
+            const int32_t i = wf_fetch(need, &counters[1], cb, ce);
             if (need) {
                 if (i < count) {
                     slot = list[i];
@@ -341,26 +380,32 @@ __global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_shadow(SceneK S, WfPa
 }
 
 template <bool UC, bool COUNT>
-__global__ __launch_bounds__(256, PT_WALK_WAVES) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
+__global__ __launch_bounds__(256, PT_CLOSEST_WAVES) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
                                                     WfClosestQ* __restrict__ CQ,
                                                     const int32_t* __restrict__ list, int32_t* counters,
-                                                    int32_t thr, unsigned long long* wc) {
+                                                    int32_t thr, unsigned long long* wc,
+                                                    int* __restrict__ ovf_ref,
+                                                    uint16_t* __restrict__ ovf_dist) {
     uint32_t c_q = 0, c_nodes = 0, c_units = 0;
     const int32_t count = counters[0];   // [count, head]
+    int32_t cb = 0, ce = 0;   // this wave's claimed list positions (wf_fetch)
     int32_t slot = -1;
     bool exhausted = false;
     ClosestAcc ca = closest_init();
     ClosestTrav T;
-    // the walk stack in shared memory: kWalkStack x 6 B per lane
-    __shared__ int sref[kWalkStack][256];
-    __shared__ uint16_t sdist[kWalkStack][256];
-    const ClosestStack K{&sref[0][threadIdx.x], &sdist[0][threadIdx.x], 256};
+    // the walk stack: its top kWalkStackLds entries in shared memory (6 B
+    // each per lane), the rest in global memory
+    __shared__ int sref[kWalkStackLds][256];
+    __shared__ uint16_t sdist[kWalkStackLds][256];
+    const int lanes = (int)gridDim.x * 256, gl = (int)(blockIdx.x * 256u + threadIdx.x);
+    const ClosestStack K{&sref[0][threadIdx.x], &sdist[0][threadIdx.x], 256, ovf_ref + gl,
+                         ovf_dist + gl, lanes, kWalkStackLds};
     T.ref = kNoRef;
     int pl = kNoRef, pl2 = kNoRef;   // postponed leaves
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
-            const int32_t i = wf_fetch(need, &counters[1]);
+            const int32_t i = wf_fetch(need, &counters[1], cb, ce);
             if (need) {
                 if (i < count) {
                     slot = list[i];
@@ -481,7 +526,7 @@ struct pt_scene {
     // wavefront path (BVH scenes): path records, query records, query lists
     // and counters, one allocation grown on demand
     void* wf = nullptr;
-    size_t wf_slots = 0;
+    size_t wf_bytes = 0;
     hipStream_t wf_side = nullptr;             // the closest walks run beside the shadow walks
     hipEvent_t wf_ev_shade = nullptr, wf_ev_walk = nullptr;
     std::vector<hipEvent_t> prof_ev;           // PT_FLAG_KERNEL_TIMES
@@ -704,8 +749,14 @@ static uint32_t choose_split(uint64_t image_pixels, int32_t spp, bool bvh) {
 #ifndef PT_WF_THR_CLOSEST
 #define PT_WF_THR_CLOSEST 24
 #endif
-#ifndef PT_WF_BLOCKS_PER_CU
-#define PT_WF_BLOCKS_PER_CU 3
+#ifndef PT_WF_SHADOW_BLOCKS_PER_CU
+#define PT_WF_SHADOW_BLOCKS_PER_CU 4
+#endif
+#ifndef PT_WF_CLOSEST_BLOCKS_PER_CU
+#define PT_WF_CLOSEST_BLOCKS_PER_CU 5
+#endif
+#ifndef PT_WF_CONCURRENT   // the two walks of a step on two streams
+#define PT_WF_CONCURRENT 1
 #endif
 
 // The wavefront render of a BVH scene (pt_wavefront.h): per step one shade
@@ -718,14 +769,24 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     const size_t slots = (size_t)grid.x * 256;
     const size_t sz_w = slots * sizeof(WfPath), sz_s = slots * sizeof(WfShadowQ),
                  sz_c = slots * sizeof(WfClosestQ), sz_l = 2 * slots * sizeof(int32_t);
+    const unsigned sh_blocks =
+        std::max(1u, std::min<unsigned>(grid.x, (unsigned)PT_WF_SHADOW_BLOCKS_PER_CU * (unsigned)s->n_cu));
+    const unsigned cl_blocks =
+        std::max(1u, std::min<unsigned>(grid.x, (unsigned)PT_WF_CLOSEST_BLOCKS_PER_CU * (unsigned)s->n_cu));
+    // walk-stack overflow (entries below the shared-memory part): 4 B per
+    // entry and shadow lane, 4 + 2 B per entry and closest lane
+    const size_t ovf_n = (size_t)kWalkStackGlobal;
+    const size_t sz_os = ovf_n * sh_blocks * 256 * 4, sz_ocr = ovf_n * cl_blocks * 256 * 4,
+                 sz_ocd = ovf_n * cl_blocks * 256 * 2;
     const size_t off_s = sz_w, off_c = off_s + sz_s, off_l = off_c + sz_c, off_n = off_l + sz_l;
-    const size_t need = off_n + 256;
-    if (slots > s->wf_slots) {
+    const size_t off_os = off_n + 256, off_ocr = off_os + sz_os, off_ocd = off_ocr + sz_ocr;
+    const size_t need = off_ocd + sz_ocd + 256;
+    if (need > s->wf_bytes) {
         if (s->wf) (void)hipFree(s->wf);
         s->wf = nullptr;
-        s->wf_slots = 0;
+        s->wf_bytes = 0;
         if (hipMalloc(&s->wf, need) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc wavefront buffers");
-        s->wf_slots = slots;
+        s->wf_bytes = need;
     }
     if (!s->wf_side) {
         HIPCHK(hipStreamCreateWithFlags(&s->wf_side, hipStreamNonBlocking));
@@ -738,8 +799,9 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     WfClosestQ* CQ = (WfClosestQ*)(b + off_c);
     int32_t* lists = (int32_t*)(b + off_l);
     int32_t* counters = (int32_t*)(b + off_n);
-    const unsigned wf_blocks =
-        std::max(1u, std::min<unsigned>(grid.x, (unsigned)PT_WF_BLOCKS_PER_CU * (unsigned)s->n_cu));
+    int* ovf_s = (int*)(b + off_os);
+    int* ovf_cr = (int*)(b + off_ocr);
+    uint16_t* ovf_cd = (uint16_t*)(b + off_ocd);
     const int32_t per_slot = (R.spp + (int32_t)R.split - 1) / (int32_t)R.split;
     const int32_t steps = per_slot * R.bounces + 2;
     const bool wcount = (flags & PT_FLAG_WALK_COUNT) != 0 && stats;
@@ -761,21 +823,21 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     auto closest_walk = [&](hipStream_t on) {
         const int32_t* l = lists + slots;
         if (s->dev.bunitc) {
-            if (wcount) hipLaunchKernelGGL((k_wf_closest<true, true>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3);
-            else hipLaunchKernelGGL((k_wf_closest<true, false>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3);
+            if (wcount) hipLaunchKernelGGL((k_wf_closest<true, true>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd);
+            else hipLaunchKernelGGL((k_wf_closest<true, false>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd);
         } else {
-            if (wcount) hipLaunchKernelGGL((k_wf_closest<false, true>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3);
-            else hipLaunchKernelGGL((k_wf_closest<false, false>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3);
+            if (wcount) hipLaunchKernelGGL((k_wf_closest<false, true>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd);
+            else hipLaunchKernelGGL((k_wf_closest<false, false>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd);
         }
     };
     auto shadow_walk = [&](hipStream_t on) {
         const int32_t* l = lists;
         if (s->dev.bunitc) {
-            if (wcount) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc);
-            else hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc);
+            if (wcount) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc, ovf_s);
+            else hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc, ovf_s);
         } else {
-            if (wcount) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc);
-            else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(wf_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc);
+            if (wcount) hipLaunchKernelGGL((k_wf_shadow<false, true>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc, ovf_s);
+            else hipLaunchKernelGGL((k_wf_shadow<false, false>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc, ovf_s);
         }
     };
     HIPCHK(hipEventRecord(s->ev0, st));
@@ -788,16 +850,19 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
         if (step + 1 < steps) {
             // the two walks only read the shade step's output and write
             // disjoint records: the closest walks run on a side stream
-            HIPCHK(hipEventRecord(s->wf_ev_shade, st));
-            HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
-            HIPCHK(mark(step, 2, 0, s->wf_side));
-            closest_walk(s->wf_side);
-            HIPCHK(mark(step, 2, 1, s->wf_side));
-            HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
+            hipStream_t cs = PT_WF_CONCURRENT ? s->wf_side : st;
+            if (PT_WF_CONCURRENT) {
+                HIPCHK(hipEventRecord(s->wf_ev_shade, st));
+                HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
+            }
+            HIPCHK(mark(step, 2, 0, cs));
+            closest_walk(cs);
+            HIPCHK(mark(step, 2, 1, cs));
+            if (PT_WF_CONCURRENT) HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
             HIPCHK(mark(step, 1, 0, st));
             shadow_walk(st);
             HIPCHK(mark(step, 1, 1, st));
-            HIPCHK(hipStreamWaitEvent(st, s->wf_ev_walk, 0));
+            if (PT_WF_CONCURRENT) HIPCHK(hipStreamWaitEvent(st, s->wf_ev_walk, 0));
         }
     }
     hipLaunchKernelGGL(k_wf_final, grid, dim3(256), 0, st, s->dev, R, (const WfPath*)W, out_dev);

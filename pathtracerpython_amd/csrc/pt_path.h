@@ -337,6 +337,126 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
     }
 }
 
+// The f64 decisions of a unit's ambiguous tests (bits of amb, see
+// fused_unit).  Out of line in the render kernels: the block is large (an
+// eval64 per bit) and runs for few waves, so the unit loop does not carry its
+// registers and code.
+#ifndef PT_FALLBACK_NOINLINE
+#define PT_FALLBACK_NOINLINE 0
+#endif
+#if PT_FALLBACK_NOINLINE && defined(__HIP_DEVICE_COMPILE__)
+#define PT_FALLBACK_ATTR __device__ __attribute__((noinline))
+#else
+#define PT_FALLBACK_ATTR PT_HD
+#endif
+#ifndef PT_FALLBACK_LOOP
+#define PT_FALLBACK_LOOP 0
+#endif
+template <bool FORCE64, bool COUNT, bool MARGIN>
+PT_FALLBACK_ATTR void fused_fallback(const SceneK& S, const UnitF& U, uint32_t amb, ShadowSet* sh,
+                                     ClosestAcc* ca, const Spill& sp, Counters* cnt, float* oc) {
+    const D3 P = sp.get3(kSpP);
+#if PT_FALLBACK_LOOP
+    if (!FORCE64) {
+        // one eval64 site: each lane walks its own ambiguous tests in bit
+        // order (shadow ray k, triangle i at bit 2k+i; the closest ray's at
+        // 6+i), the order of the nested loops below
+        uint32_t bits = amb;
+        while (bits) {
+            const int bi = __builtin_ctz(bits);
+            bits &= bits - 1u;
+            const int i = bi & 1, k = bi >> 1;
+            const int t = U.t[i];
+            if (bi < 6) {   // shadow ray k
+                const bool occk = MARGIN ? ((k == 0 ? oc[0] : (k == 1 ? oc[1] : oc[2])) > 0.0f)
+                                         : (k == 0 ? sh->occ[0] : (k == 1 ? sh->occ[1] : sh->occ[2]));
+                const int firstk = k == 0 ? sh->first[0] : (k == 1 ? sh->first[1] : sh->first[2]);
+                // decided meanwhile (a lower occluder of this unit, or occlusion)?
+                if (k == kLightSamples - 1 ? ((COUNT ? t : U.obj) >= sh->key2)
+                                           : (COUNT ? (t >= firstk) : occk))
+                    continue;
+                bump<COUNT>(cnt, &Counters::fallbacks, 1);
+                const D3 L = sp.get3(kSpL + 3 * k);
+                D3 Q;
+                double sqd;
+                if (eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
+                    sqd < squared_dist(P, L)) {
+                    if (COUNT && t < firstk) {
+                        if (k == 0) sh->first[0] = t;
+                        else if (k == 1) sh->first[1] = t;
+                        else sh->first[2] = t;
+                    }
+                    if (k == kLightSamples - 1) {
+                        sh->key2 = COUNT ? t : U.obj;
+                        sh->leak = U.obj;
+                    }
+                    if (MARGIN) {
+                        if (k == 0) oc[0] = 1.0f;
+                        else if (k == 1) oc[1] = 1.0f;
+                        else oc[2] = 1.0f;
+                    } else {
+                        if (k == 0) sh->occ[0] = true;
+                        else if (k == 1) sh->occ[1] = true;
+                        else sh->occ[2] = true;
+                    }
+                }
+            } else {   // the closest ray
+                bump<COUNT>(cnt, &Counters::fallbacks, 1);
+                D3 Q;
+                double sqd;
+                float a = INFINITY, b = INFINITY;
+                if (eval64(S.trid[t], P, unit(sp.get3(kSpNd)), &Q, &sqd) && sqd > kZero) {
+                    const float sq = sqrtf((float)sqd);   // |t| to ~1e-7; brackets are 1e-6
+                    a = sq * (1.0f - 1e-6f);
+                    b = sq * (1.0f + 1e-6f);
+                }
+                closest_add(ca, t, a, b);
+            }
+        }
+        return;
+    }
+#endif
+    for (int k = 0; k < kLightSamples; ++k) {
+        for (int i = 0; i < 2; ++i) {
+            if (!((amb >> (2 * k + i)) & 1u)) continue;
+            const int t = U.t[i];
+            // decided meanwhile (a lower occluder of this unit, or occlusion)?
+            if (k == kLightSamples - 1 ? ((COUNT ? t : U.obj) >= sh->key2)
+                                       : (COUNT ? (t >= sh->first[k])
+                                                : (MARGIN ? oc[k] > 0.0f : sh->occ[k])))
+                continue;
+            D3 Q;
+            double sqd;
+            if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
+            const D3 L = sp.get3(kSpL + 3 * k);
+            if (eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
+                sqd < squared_dist(P, L)) {
+                if (COUNT && t < sh->first[k]) sh->first[k] = t;
+                if (k == kLightSamples - 1) {
+                    sh->key2 = COUNT ? t : U.obj;
+                    sh->leak = U.obj;
+                }
+                if (MARGIN) oc[k] = 1.0f;
+                else sh->occ[k] = true;
+            }
+        }
+    }
+    for (int i = 0; i < 2; ++i) {
+        if (!((amb >> (6 + i)) & 1u)) continue;
+        const int t = U.t[i];
+        D3 Q;
+        double sqd;
+        bump<COUNT>(cnt, &Counters::fallbacks, 1);
+        float a = INFINITY, b = INFINITY;
+        if (eval64(S.trid[t], P, unit(sp.get3(kSpNd)), &Q, &sqd) && sqd > kZero) {
+            const float sq = sqrtf((float)sqd);   // |t| to ~1e-7; brackets are 1e-6
+            a = sq * (1.0f - 1e-6f);
+            b = sq * (1.0f + 1e-6f);
+        }
+        closest_add(ca, t, a, b);
+    }
+}
+
 // One plane unit against the 3 shadow rays and the next ray's closest hit,
 // all from the same origin (the fused per-bounce pass).  Every verdict is
 // computed branch-free; ambiguous tests are only recorded as bits and
@@ -411,48 +531,10 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
                     c ? p.at + p.dt : INFINITY);
         amb |= (a0 ? 64u : 0u) | (a1 ? 128u : 0u);
     }
-    if (amb) {   // rare (FORCE64: every shadow test) — decide in f64
-        const D3 P = sp.get3(kSpP);
-        for (int k = 0; k < kLightSamples; ++k) {
-            for (int i = 0; i < 2; ++i) {
-                if (!((amb >> (2 * k + i)) & 1u)) continue;
-                const int t = U.t[i];
-                // decided meanwhile (a lower occluder of this unit, or occlusion)?
-                if (k == kLightSamples - 1 ? ((COUNT ? t : U.obj) >= sh->key2)
-                                           : (COUNT ? (t >= sh->first[k])
-                                                    : (MARGIN ? oc[k] > 0.0f : sh->occ[k])))
-                    continue;
-                D3 Q;
-                double sqd;
-                if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
-                const D3 L = sp.get3(kSpL + 3 * k);
-                if (eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
-                    sqd < squared_dist(P, L)) {
-                    if (COUNT && t < sh->first[k]) sh->first[k] = t;
-                    if (k == kLightSamples - 1) {
-                        sh->key2 = COUNT ? t : U.obj;
-                        sh->leak = U.obj;
-                    }
-                    if (MARGIN) oc[k] = 1.0f;
-                    else sh->occ[k] = true;
-                }
-            }
-        }
-        for (int i = 0; i < 2; ++i) {
-            if (!((amb >> (6 + i)) & 1u)) continue;
-            const int t = U.t[i];
-            D3 Q;
-            double sqd;
-            bump<COUNT>(cnt, &Counters::fallbacks, 1);
-            float a = INFINITY, b = INFINITY;
-            if (eval64(S.trid[t], P, unit(sp.get3(kSpNd)), &Q, &sqd) && sqd > kZero) {
-                const float sq = sqrtf((float)sqd);   // |t| to ~1e-7; brackets are 1e-6
-                a = sq * (1.0f - 1e-6f);
-                b = sq * (1.0f + 1e-6f);
-            }
-            closest_add(ca, t, a, b);
-        }
-    }
+#ifdef PT_ABL_NOAMB   // timing ablation only (wrong results)
+    if (!FORCE64) amb = 0;
+#endif
+    if (amb) fused_fallback<FORCE64, COUNT, MARGIN>(S, U, amb, sh, ca, sp, cnt, oc);   // rare (FORCE64: every shadow test) — decide in f64
 }
 
 template <bool COUNT>
@@ -606,6 +688,19 @@ struct ClosestStack {
     int* ref;
     uint16_t* dist;
     int stride;
+    // the walk kernels keep the first nl entries in LDS (ref / dist, stride
+    // `stride`) and the deeper ones, rarely touched, in global memory (gref /
+    // gdist, stride gs)
+    int* gref = nullptr;
+    uint16_t* gdist = nullptr;
+    int gs = 0;
+    int nl = 1 << 30;
+    PT_HD void set(int i, int r, uint16_t d) const {
+        if (i < nl) { ref[i * stride] = r; dist[i * stride] = d; }
+        else { gref[(i - nl) * gs] = r; gdist[(i - nl) * gs] = d; }
+    }
+    PT_HD int get_ref(int i) const { return i < nl ? ref[i * stride] : gref[(i - nl) * gs]; }
+    PT_HD uint16_t get_dist(int i) const { return i < nl ? dist[i * stride] : gdist[(i - nl) * gs]; }
 };
 struct ClosestStackLocal {
     int ref[kBvhStack];
@@ -625,10 +720,7 @@ PT_HD float dist_up16(uint16_t h) {
 }
 PT_HD void ctrav_push(ClosestTrav& T, const ClosestStack& K, int r, float d) {
     if (T.tref != kNoRef) {
-        K.ref[T.top * K.stride] = T.tref;
-#ifndef PT_CSTACK_NODIST
-        K.dist[T.top * K.stride] = dist_down16(T.tdist);
-#endif
+        K.set(T.top, T.tref, dist_down16(T.tdist));
         ++T.top;
     }
     T.tref = r;
@@ -640,12 +732,8 @@ PT_HD int ctrav_pop(ClosestTrav& T, const ClosestStack& K, float bound) {   // n
         const float d = T.tdist;
         if (T.top > 0) {
             --T.top;
-            T.tref = K.ref[T.top * K.stride];
-#ifndef PT_CSTACK_NODIST
-            T.tdist = dist_up16(K.dist[T.top * K.stride]);
-#else
-            T.tdist = 0.0f;
-#endif
+            T.tref = K.get_ref(T.top);
+            T.tdist = dist_up16(K.get_dist(T.top));
         } else {
             T.tref = kNoRef;
         }
@@ -757,14 +845,22 @@ struct ShadowTrav {
 struct ShadowStack {
     int* e;
     int stride;
-    PT_HD int& operator[](int i) const { return e[i * stride]; }
+    // entries from nl on in global memory (g, stride gs): see ClosestStack
+    int* g = nullptr;
+    int gs = 0;
+    int nl = 1 << 30;
+    PT_HD int get(int i) const { return i < nl ? e[i * stride] : g[(i - nl) * gs]; }
+    PT_HD void set(int i, int v) const {
+        if (i < nl) e[i * stride] = v;
+        else g[(i - nl) * gs] = v;
+    }
 };
 template <bool COUNT>
 PT_HD int strav_pop(ShadowTrav& T, const ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
     const uint32_t open = shadow_open<COUNT>(S, sh);
     while (T.tc != 0) {
         const int e = T.tc;
-        T.tc = T.top > 0 ? K[--T.top] : 0;
+        T.tc = T.top > 0 ? K.get(--T.top) : 0;
         T.rays = (uint32_t)e & open & 7u;
         if (T.rays) return e >> 3;
     }
@@ -811,7 +907,7 @@ PT_HD void strav_node(ShadowTrav& T, const ShadowStack& K, const SceneK& S, cons
     const uint32_t mn = near0 ? m0 : m1, mf = near0 ? m1 : m0;
     const int rn = near0 ? C.c0 : C.c1, rf = near0 ? C.c1 : C.c0;
     if (mf) {
-        if (T.tc != 0) K[T.top++] = T.tc;
+        if (T.tc != 0) K.set(T.top++, T.tc);
         T.tc = (int)(((uint32_t)rf << 3) | mf);
     }
     if (mn) {
@@ -918,7 +1014,7 @@ PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, con
 #pragma unroll
     for (int c = 3; c >= 1; --c) {
         if (m[c]) {
-            if (T.tc != 0) K[T.top++] = T.tc;
+            if (T.tc != 0) K.set(T.top++, T.tc);
             T.tc = (int)(((uint32_t)r[c] << 3) | m[c]);
         }
     }
@@ -1130,8 +1226,12 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
             for (int u = 0; u < S.n_obj_unit; ++u) {
                 const UnitF U = S.unit[u];
                 const OriginU O = origin_u(U, o32u);
+#ifdef PT_ABL_NOSHADOW   // timing ablation only (wrong results)
+                const bool do_shadow = false;
+#else
                 const bool do_shadow =
                     PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));
+#endif
                 fused_unit<FORCE64, COUNT, true>(S, U, O, U.grp == ogrp, do_shadow, any_trace,
                                                  &sh, n32, &ca, sp, cnt, 15u, oc);
             }

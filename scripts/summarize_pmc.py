@@ -13,6 +13,7 @@ for d in dirs:
             meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                                       "Scratch_Size", "VGPR_Count", "SGPR_Count")}
 res = {"kernel": meta, "per_dispatch_median": {k: statistics.median(v) for k, v in agg.items()},
+       "sum_over_dispatches": {k: sum(v) for k, v in agg.items()},
        "dispatches": {k: len(v) for k, v in agg.items()}}
 if "FETCH_SIZE" in agg or "WRITE_SIZE" in agg:
     fk = res["per_dispatch_median"].get("FETCH_SIZE", 0.0)

@@ -95,12 +95,35 @@ int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
 // steps_out (optional): shade steps that found work.
 // walk_stats (optional, int64[8]): shadow queries, node visits, leaves,
 // leaf units; the same for the closest walks.
+// depth_hist (optional, int64[2][32]): node visits of the shadow / closest
+// walks by QNode depth (root = 0)
+int hc_render_wavefront2(const pt_scene_desc* d, const pt_render_params* p, double* out,
+                         int32_t* steps_out, int64_t* walk_stats, int64_t* depth_hist);
 int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, double* out,
                         int32_t* steps_out, int64_t* walk_stats) {
+    return hc_render_wavefront2(d, p, out, steps_out, walk_stats, nullptr);
+}
+int hc_render_wavefront2(const pt_scene_desc* d, const pt_render_params* p, double* out,
+                         int32_t* steps_out, int64_t* walk_stats, int64_t* depth_hist) {
     int64_t ws[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HostScene H;
     if (!prepare_scene(d, &H).empty()) return -1;
     bind_host(&H);
+    std::vector<int> qdepth(H.qnode.size(), 0);
+    if (depth_hist && H.k.qroot >= 0) {   // depth of every QNode (refs point deeper)
+        std::vector<int> st{H.k.qroot};
+        while (!st.empty()) {
+            const int q = st.back();
+            st.pop_back();
+            for (int c = 0; c < 4; ++c) {
+                const int r = H.qnode[q].ref[c];
+                if (r >= 0) { qdepth[r] = qdepth[q] + 1; st.push_back(r); }
+            }
+        }
+    }
+    auto hist = [&](int kind, int ref) {
+        if (depth_hist && ref >= 0) ++depth_hist[kind * 32 + std::min(qdepth[ref], 31)];
+    };
     if (H.k.n_bnode == 0 || H.k.n_qnode == 0 || H.k.qstack > kBvhStack) return -3;
     int32_t first, rows;
     if (!band_layout(p, &first, &rows)) return -2;
@@ -154,7 +177,7 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
                 strav_init<false>(T, H.k, o32, ogrp, &sh, H.k.qroot);
                 ++ws[0];
                 while (T.ref != kNoRef) {   // strav_step over the 4-wide nodes, counted
-                    while (T.ref >= 0) { strav_qnode<false>(T, K, H.k, &sh); ++ws[1]; }
+                    while (T.ref >= 0) { hist(0, T.ref); strav_qnode<false>(T, K, H.k, &sh); ++ws[1]; }
                     if (T.ref != kNoRef) {
                         ++ws[2];
                         ws[3] += (~T.ref) & 7;
@@ -177,7 +200,7 @@ int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, doubl
                            H.k.qroot);
                 ++ws[4];
                 while (T.ref != kNoRef) {   // ctrav_step, counted
-                    while (T.ref >= 0) { ctrav_qnode(T, K, H.k, &ca); ++ws[5]; }
+                    while (T.ref >= 0) { hist(1, T.ref); ctrav_qnode(T, K, H.k, &ca); ++ws[5]; }
                     if (T.ref != kNoRef) {
                         ++ws[6];
                         ws[7] += (~T.ref) & 7;

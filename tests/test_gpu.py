@@ -298,7 +298,11 @@ def test_render_multi_bands_bitwise(cornell):
         band = m.render(W, H, 16, 4, 3, out_f64=True, row_begin=5, row_end=40)
         assert np.array_equal(band, ref[H - 40:H - 5])
         _, mst = m.render(W, H, 16, 4, 3, out_f64=True, stats=True)
-        assert mst == st
+        # the reference-semantics counters add up over the bands (the f64
+        # fallback counts are diagnostics that depend on wave composition)
+        diag = ("f64_fallbacks", "f64_rescans")
+        assert {k: v for k, v in mst.items() if k not in diag} == \
+            {k: v for k, v in st.items() if k not in diag}
 
 
 def test_wavefront_walk_counts_and_times(k5small):
