@@ -643,8 +643,9 @@ PT_HD float box_dist(F3 l, F3 h, F3 inv, float R) {   // INFINITY: not within |t
     const float az = l.z * inv.z, bz = h.z * inv.z;
     const float tmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
     const float tmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-    const float d = tmin > 0.0f ? tmin : (tmax < 0.0f ? -tmax : 0.0f);
-    return ((tmin <= tmax) & (tmin <= R) & (tmax >= -R)) ? d : INFINITY;
+    // the smallest |t| in [tmin, tmax]; within |t| <= R exactly when <= R
+    const float d = fmaxf(fmaxf(tmin, -tmax), 0.0f);
+    return ((tmin <= tmax) & (d <= R)) ? d : INFINITY;
 }
 PT_HD float node_dist(const SceneK& S, int i, F3 o32, F3 inv, float R) {
     const BNode N = S.bnode[i];
@@ -972,6 +973,37 @@ PT_HD void q_box(const QNode& Q, int c, const float st[3], F3 o, F3* l, F3* h) {
     h->y = fmaf(q_byte(Q.qhi[1], c), st[1], Q.org[1]) - o.y;
     h->z = fmaf(q_byte(Q.qhi[2], c), st[2], Q.org[2]) - o.z;
 }
+// A line's slab parameters on a node's grid: child c's bound q (in grid
+// steps) lies at line parameter t = q A + B with A = step inv (exact: the
+// step is a power of two) and B = (org - o) inv, one fma per bound instead of
+// decoding the box and subtracting the origin (q_box).  Rounding: B errs by
+// ~2u |org - o| |inv| and the fma by u|t|, i.e. a few u X in distance along
+// the line, far inside the boxes' 64 u X inflation (pt_prepare.h), so the
+// test stays conservative (hc_qbvh_check).
+#ifndef PT_QLINE
+#define PT_QLINE 1
+#endif
+struct QLine { float A[3], B[3]; };
+PT_HD QLine q_line(const QNode& Q, const float st[3], F3 o, F3 inv) {
+    QLine L;
+    L.A[0] = st[0] * inv.x; L.B[0] = (Q.org[0] - o.x) * inv.x;
+    L.A[1] = st[1] * inv.y; L.B[1] = (Q.org[1] - o.y) * inv.y;
+    L.A[2] = st[2] * inv.z; L.B[2] = (Q.org[2] - o.z) * inv.z;
+    return L;
+}
+// child c: the smallest |t| of the (two-sided) line inside its box, INFINITY
+// when the box is not met within |t| <= R.  max(tmin, -tmax, 0) is that
+// distance (tmin > 0: tmin; tmax < 0: -tmax; else 0), and the interval meets
+// [-R, R] exactly when it is <= R.
+PT_HD float q_child_dist(const QNode& Q, int c, const QLine& L, float R) {
+    const float x0 = fmaf(q_byte(Q.qlo[0], c), L.A[0], L.B[0]), x1 = fmaf(q_byte(Q.qhi[0], c), L.A[0], L.B[0]);
+    const float y0 = fmaf(q_byte(Q.qlo[1], c), L.A[1], L.B[1]), y1 = fmaf(q_byte(Q.qhi[1], c), L.A[1], L.B[1]);
+    const float z0 = fmaf(q_byte(Q.qlo[2], c), L.A[2], L.B[2]), z1 = fmaf(q_byte(Q.qhi[2], c), L.A[2], L.B[2]);
+    const float tmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+    const float tmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+    const float d = fmaxf(fmaxf(tmin, -tmax), 0.0f);
+    return ((tmin <= tmax) & (d <= R)) ? d : INFINITY;
+}
 // 4 (distance, ref, rays) triples in ascending distance (sorting network)
 PT_HD void q_sort4(float d[4], int r[4], uint32_t m[4]) {
     auto cs = [&](int i, int j) {
@@ -992,16 +1024,28 @@ PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, con
     float d[4];
     int r[4];
     uint32_t m[4];
+#if PT_QLINE
+    QLine L[kLightSamples];
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) L[k] = q_line(Q, st, T.o32, T.inv[k]);
+#endif
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
+#if !PT_QLINE
         F3 l, h;
         q_box(Q, c, st, T.o32, &l, &h);
+#endif
         float dc = INFINITY;
         uint32_t mc = 0;
 #pragma unroll
         for (int k = 0; k < kLightSamples; ++k) {
-            if (!((T.rays >> k) & 1u)) continue;
-            const float e = box_dist(l, h, T.inv[k], sh->hhi[k]);
+            // every ray computed, closed ones masked (no per-ray branch)
+#if PT_QLINE
+            const float e0 = q_child_dist(Q, c, L[k], sh->hhi[k]);
+#else
+            const float e0 = box_dist(l, h, T.inv[k], sh->hhi[k]);
+#endif
+            const float e = ((T.rays >> k) & 1u) ? e0 : INFINITY;
             mc |= e < INFINITY ? 1u << k : 0u;
             dc = fminf(dc, e);
         }
@@ -1032,12 +1076,20 @@ PT_HD void ctrav_qnode(ClosestTrav& T, const ClosestStack& K, const SceneK& S, c
     float d[4];
     int r[4];
     uint32_t m[4];
+#if PT_QLINE
+    const QLine L = q_line(Q, st, T.o32, T.inv);
+#endif
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
+        r[c] = Q.ref[c];
+#if PT_QLINE
+        const float e = q_child_dist(Q, c, L, ca->b1);
+#else
         F3 l, h;
         q_box(Q, c, st, T.o32, &l, &h);
-        r[c] = Q.ref[c];
-        d[c] = r[c] != kNoRef ? box_dist(l, h, T.inv, ca->b1) : INFINITY;
+        const float e = box_dist(l, h, T.inv, ca->b1);
+#endif
+        d[c] = r[c] != kNoRef ? e : INFINITY;
         m[c] = 0;
     }
     q_sort4(d, r, m);

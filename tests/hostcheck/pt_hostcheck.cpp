@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <random>
 
 #include "../../pathtracerpython_amd/csrc/pt_path.h"
@@ -413,6 +414,83 @@ int hc_bvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t*
         }
     }
     out[0] = bad; out[1] = missed; out[2] = checked; out[3] = N;
+    return 0;
+}
+
+// 4-wide walk check (QNode, the wavefront walks' child test): random lines as
+// in hc_bvh_check; for every BVH triangle the f64 line meets at sqd, a walk
+// of the QNode tree that enters every child whose test (the kernels'
+// q_child_dist / box_dist) passes within |t| <= sqrt(sqd)(1 + 1e-6) must
+// reach that triangle's leaf.  out: [0] missed hits, [1] hits checked,
+// [2] QNodes.
+int hc_qbvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t* out) {
+    HostScene H;
+    if (!prepare_scene(d, &H).empty()) return -1;
+    bind_host(&H);
+    const SceneK& K = H.k;
+    int64_t missed = 0, checked = 0;
+    if (K.n_qnode == 0) { out[0] = out[1] = 0; out[2] = 0; return 0; }
+    // leaf of every BVH unit: the leaf codes in the QNode refs
+    std::vector<int> leaf_of(K.n_bunit, 0);
+    for (int q = 0; q < K.n_qnode; ++q)
+        for (int c = 0; c < 4; ++c) {
+            const int r = H.qnode[q].ref[c];
+            if (r <= -2) {
+                const int code = ~r, u0 = code >> 3, nu = code & 7;
+                for (int i = 0; i < nu; ++i) leaf_of[u0 + i] = r;
+            }
+        }
+    std::mt19937_64 rng(seed);
+    std::uniform_real_distribution<double> U01(0.0, 1.0);
+    std::vector<int> reached;
+    for (int64_t r = 0; r < n_rays; ++r) {
+        D3 o;
+        if (r % 4 == 0) {
+            o = ld3(K.eye);
+        } else {
+            const UnitF& U = H.bunit[(size_t)(U01(rng) * K.n_bunit) % K.n_bunit];
+            const TriD& T = H.trid[U.t[0]];
+            double a = U01(rng), b = U01(rng);
+            if (a + b > 1) { a = 1 - a; b = 1 - b; }
+            o = ld3(T.v1) * (1 - a - b) + ld3(T.v2) * a + ld3(T.v3) * b;
+        }
+        const D3 dn = unit(d3(U01(rng) - 0.5, U01(rng) - 0.5, U01(rng) - 0.5));
+        const F3 o32 = to_f3(o - ld3(K.center)), inv = rcp_dir(to_f3(dn));
+        for (int q = 0; q < K.n_bunit; ++q) {
+            const UnitF& U = H.bunit[q];
+            for (int m = 0; m < U.count; ++m) {
+                D3 Q; double sqd;
+                if (!eval64(H.trid[U.t[m]], o, dn, &Q, &sqd)) continue;
+                const float R = (float)(sqrt(sqd) * (1 + 1e-6));
+                ++checked;
+                reached.clear();
+                std::vector<int> st{K.qroot};
+                while (!st.empty()) {
+                    const int n = st.back();
+                    st.pop_back();
+                    if (n <= -2) { reached.push_back(n); continue; }
+                    const QNode& N = H.qnode[n];
+                    const float step[3] = {q_step(N.ex, 0), q_step(N.ex, 1), q_step(N.ex, 2)};
+#if PT_QLINE
+                    const QLine L = q_line(N, step, o32, inv);
+#endif
+                    for (int c = 0; c < 4; ++c) {
+                        if (N.ref[c] == kNoRef) continue;
+#if PT_QLINE
+                        const float e = q_child_dist(N, c, L, R);
+#else
+                        F3 l, h;
+                        q_box(N, c, step, o32, &l, &h);
+                        const float e = box_dist(l, h, inv, R);
+#endif
+                        if (e < INFINITY) st.push_back(N.ref[c]);
+                    }
+                }
+                if (std::find(reached.begin(), reached.end(), leaf_of[q]) == reached.end()) ++missed;
+            }
+        }
+    }
+    out[0] = missed; out[1] = checked; out[2] = K.n_qnode;
     return 0;
 }
 
