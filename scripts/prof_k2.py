@@ -20,3 +20,5 @@ for i in range(n):
     torch.cuda.synchronize()
     ms.append(r.last_kernel_ms())
 print("kernel ms", ms, "Mpath/s %.1f" % (512 * 512 * 64 / min(ms) / 1e3))
+import hashlib
+print("fb sha", hashlib.sha256(tile.cpu().numpy().tobytes()).hexdigest()[:16])
