@@ -317,15 +317,15 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
         const RayPlane p = ray_plane(U, O.h, d, sh->hlo[k], sh->hhi[k]);
         float cm, nm;
         margin_plane(U, p, sh->hlo[k], sh->hhi[k], cop, &cm, &nm);
-        float c0 = -INFINITY, a0 = -INFINITY, c1 = -INFINITY, a1 = -INFINITY;
         // nm < 0 (the plane part is a certain miss; nm is never NaN, cop is
         // not) implies cm < 0, so every margin of the ray's triangles is
-        // negative or a dropped NaN: the triangle part only runs when some
-        // lane of the wave is not certainly out of range (K2 6.49 -> 6.35 ms)
-        if (PT_WAVE_ANY(!(nm < 0.0f))) {
-            margin_tri(U.tri[0], p, O.bo0, O.co0, d, cm, nm, &c0, &a0);
-            if (two) margin_tri(U.tri[1], p, O.bo1, O.co1, d, cm, nm, &c1, &a1);   // wave-uniform
-        }
+        // negative or a dropped NaN: no occlusion, no ambiguous test.  The
+        // triangle part only runs when some lane of the wave is not
+        // certainly out of range (K2 6.49 -> 6.35 ms).
+        if (!PT_WAVE_ANY(!(nm < 0.0f))) continue;
+        float c0, a0, c1 = -INFINITY, a1 = -INFINITY;
+        margin_tri(U.tri[0], p, O.bo0, O.co0, d, cm, nm, &c0, &a0);
+        if (two) margin_tri(U.tri[1], p, O.bo1, O.co1, d, cm, nm, &c1, &a1);   // wave-uniform
         const float old = oc[k];
         const float c = fmaxf(c0, c1);
         oc[k] = fmaxf(old, c);
