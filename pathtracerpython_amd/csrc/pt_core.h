@@ -69,7 +69,8 @@ struct alignas(16) UnitF {   // 128 B: two s_load_dwordx16
     int32_t grp, count;
     int32_t obj;             // the members' object (one per unit)
     int32_t t[2];            // member triangle indices in scene order
-    int32_t pad;
+    int32_t quad;            // 1: a parallelogram pair (tri[0] labelled for quad_m,
+                             // pt_path.h), 0: a single triangle, -1: another pair
     TriB tri[2];
 };
 static_assert(sizeof(UnitF) == 128, "UnitF is two scalar x16 loads");
@@ -270,6 +271,25 @@ PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t 
     }
 }
 
+// One Philox4x32-10 block: slots 4 blk .. 4 blk + 3 of (pixel, sample, bounce)
+PT_HD void rng_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t blk,
+                     uint32_t c[4]) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    c[0] = pixel; c[1] = sample; c[2] = bounce; c[3] = blk;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[1] = (uint32_t)p1;
+        c[3] = (uint32_t)p0;
+        c[0] = n0;
+        c[2] = n2;
+    }
+}
+
 PT_HD double u_of(uint32_t w) { return (double)(w >> 8) * (1.0 / 16777216.0); }
 
 // ------------------------------------------------------------- vectors --
@@ -377,15 +397,18 @@ struct Verdict {
     bool cand;   // the reference certainly reports a usable intersection
     bool amb;    // undecided: evaluate in f64
 };
-PT_HD Verdict classify_tri(const TriB& B, const RayPlane& p, float bo, float co, F3 d) {
-    const float beta = fmaf(p.t, lin3(B.gb, d), bo);
-    const float gam = fmaf(p.t, lin3(B.gc, d), co);
-    const float m = min3f(beta, gam, (1.0f - beta) - gam);
+// the verdict of a test from its weight minimum m
+PT_HD Verdict verdict_m(float m, const RayPlane& p) {
     const float del = p.del;
     Verdict v;
     v.cand = p.rcand & (m > del);
     v.amb = !(p.rmiss | (m < -del)) & !v.cand;
     return v;
+}
+PT_HD Verdict classify_tri(const TriB& B, const RayPlane& p, float bo, float co, F3 d) {
+    const float beta = fmaf(p.t, lin3(B.gb, d), bo);
+    const float gam = fmaf(p.t, lin3(B.gc, d), co);
+    return verdict_m(min3f(beta, gam, (1.0f - beta) - gam), p);
 }
 PT_HD int verdict_code(Verdict v) { return v.cand ? kCand : (v.amb ? kAmb : kMiss); }
 

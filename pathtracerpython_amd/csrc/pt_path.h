@@ -248,24 +248,28 @@ struct ShadowSet {
 // The points go to the spill; f32 copies of the directions and distance
 // brackets into sh, with l_k . n for the colour.  u: the 12 uniforms (the
 // render loop draws them with rng_blocks4; the batched API passes them in).
+// light sample k of shadow_setup (u: its 4 uniforms)
+template <bool COUNT>
+PT_HD void shadow_setup_k(const SceneK& S, D3 P, D3 n, int k, double u0, double u1, double u2,
+                          double u3, ShadowSet* sh, const Spill& sp) {
+    const int li = pick_light(S, u0);
+    const D3 L = light_point(S.trid[S.light_tri[li]], u1, u2, u3);
+    sp.put3(kSpL + 3 * k, L);
+    const D3 dn = unit(L - P);                    // main.py:37-38
+    const float tl = sqrtf((float)squared_dist(P, L));   // main.py:40, to ~2e-7
+    sh->hlo[k] = tl * (1.0f - 1e-6f);
+    sh->hhi[k] = tl * (1.0f + 1e-6f);
+    sh->d32[k] = to_f3(dn);
+    sh->ln[k] = dot(dn, n);
+    sh->occ[k] = false;
+    sh->first[k] = S.n_tri;
+}
 template <bool COUNT>
 PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double u[12], ShadowSet* sh,
                         const Spill& sp) {
 #pragma unroll
-    for (int k = 0; k < kLightSamples; ++k) {
-        const double u0 = u[4 * k], u1 = u[4 * k + 1], u2 = u[4 * k + 2], u3 = u[4 * k + 3];
-        const int li = pick_light(S, u0);
-        const D3 L = light_point(S.trid[S.light_tri[li]], u1, u2, u3);
-        sp.put3(kSpL + 3 * k, L);
-        const D3 dn = unit(L - P);                    // main.py:37-38
-        const float tl = sqrtf((float)squared_dist(P, L));   // main.py:40, to ~2e-7
-        sh->hlo[k] = tl * (1.0f - 1e-6f);
-        sh->hhi[k] = tl * (1.0f + 1e-6f);
-        sh->d32[k] = to_f3(dn);
-        sh->ln[k] = dot(dn, n);
-        sh->occ[k] = false;
-        sh->first[k] = S.n_tri;
-    }
+    for (int k = 0; k < kLightSamples; ++k)
+        shadow_setup_k<COUNT>(S, P, n, k, u[4 * k], u[4 * k + 1], u[4 * k + 2], u[4 * k + 3], sh, sp);
     sh->key2 = COUNT ? S.n_tri : S.n_obj;
     sh->leak = S.n_obj - 1;
 }
@@ -279,6 +283,12 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double u[12], ShadowS
 // mode, not forced f64); ambiguous tests go to the same f64 block.
 #ifndef PT_MARGIN
 #define PT_MARGIN 1
+#endif
+#ifndef PT_QUAD
+#define PT_QUAD 1
+#endif
+#ifndef PT_RNG_PERBLOCK
+#define PT_RNG_PERBLOCK 1
 #endif
 // The candidate margins propagate NaN (v_minimum: a NaN compare is "not a
 // candidate" in classify_tri); the ambiguity margins drop it (fminf: a NaN
@@ -299,17 +309,61 @@ PT_HD void margin_plane(const UnitF& U, const RayPlane& p, float hi_lo, float hi
     *cm = nan_min(nan_min(fabsf(p.q) - U.qhi, lo - kTzHi), nan_min(hi_lo - hi, cop));
     *nm = fminf(fminf(hi - kTzLo, hi_hi - lo), cop);
 }
+// a test's margins from its weight minimum m
+PT_HD void margin_m(float m, const RayPlane& p, float cm, float nm, float* c, float* a) {
+    *c = nan_min(cm, m - p.del);
+    *a = fminf(fminf(nm, m + p.del), -*c);
+}
 PT_HD void margin_tri(const TriB& B, const RayPlane& p, float bo, float co, F3 d, float cm,
                       float nm, float* c, float* a) {
     const float beta = fmaf(p.t, lin3(B.gb, d), bo);
     const float gam = fmaf(p.t, lin3(B.gc, d), co);
-    const float m = min3f(beta, gam, (1.0f - beta) - gam);
-    *c = nan_min(cm, m - p.del);
-    *a = fminf(fminf(nm, m + p.del), -*c);
+    margin_m(min3f(beta, gam, (1.0f - beta) - gam), p, cm, nm, c, a);
+}
+
+// The render loop's form of a uniform unit (pt_prepare.h: U.quad 1 a
+// parallelogram pair, 0 a single triangle, -1 any other coplanar pair): the
+// first member's weights (beta, gamma, 1 - s), s = beta + gamma, and for a
+// parallelogram the second member's from the same forms, (s, 1 - gamma,
+// -beta) — each one rounding of an exact combination of the computed beta
+// and gamma, so the unit's del (twice a form's error bound, 16u absolute
+// slack included) covers them.  A single triangle's second test is a certain
+// miss (m1 = -inf: negative margins, never ambiguous); another pair uses the
+// second member's own forms.  Parallelograms skip the second member's forms:
+// its origin terms and 8 VALU per ray.
+struct QuadM { float m0, m1; };
+PT_HD QuadM quad_m(const UnitF& U, const RayPlane& p, const OriginU& O, F3 d) {
+    const float beta = fmaf(p.t, lin3(U.tri[0].gb, d), O.bo0);
+    const float gam = fmaf(p.t, lin3(U.tri[0].gc, d), O.co0);
+    const float s = beta + gam;
+    QuadM r;
+    r.m0 = min3f(beta, gam, 1.0f - s);
+    r.m1 = -INFINITY;
+    if (U.quad > 0) {   // wave-uniform
+        r.m1 = min3f(s, 1.0f - gam, -beta);
+    } else if (U.quad < 0) {
+        const float b1 = fmaf(p.t, lin3(U.tri[1].gb, d), O.bo1);
+        const float g1 = fmaf(p.t, lin3(U.tri[1].gc, d), O.co1);
+        r.m1 = min3f(b1, g1, (1.0f - b1) - g1);
+    }
+    return r;
+}
+// origin terms of the render loop's unit form (the second member's only for
+// a pair that is no parallelogram)
+PT_HD OriginU origin_q(const UnitF& U, F3 o) {
+    OriginU r;
+    r.h = aff3(U.n, U.cn, o);
+    r.bo0 = aff3(U.tri[0].gb, U.tri[0].cb, o);
+    r.co0 = aff3(U.tri[0].gc, U.tri[0].cc, o);
+    r.bo1 = r.co1 = 0.f;
+    if (U.quad < 0) {   // wave-uniform
+        r.bo1 = aff3(U.tri[1].gb, U.tri[1].cb, o);
+        r.co1 = aff3(U.tri[1].gc, U.tri[1].cc, o);
+    }
+    return r;
 }
 PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
                          ShadowSet* sh, float oc[kLightSamples], uint32_t* amb) {
-    const bool two = (U.count == 2);
     const float cop = coplanar ? -1.0f : INFINITY;
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
@@ -323,9 +377,16 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
         // triangle part only runs when some lane of the wave is not
         // certainly out of range (K2 6.49 -> 6.35 ms).
         if (!PT_WAVE_ANY(!(nm < 0.0f))) continue;
+#if PT_QUAD
+        const QuadM m = quad_m(U, p, O, d);
+        float c0, a0, c1, a1;
+        margin_m(m.m0, p, cm, nm, &c0, &a0);
+        margin_m(m.m1, p, cm, nm, &c1, &a1);
+#else
         float c0, a0, c1 = -INFINITY, a1 = -INFINITY;
         margin_tri(U.tri[0], p, O.bo0, O.co0, d, cm, nm, &c0, &a0);
-        if (two) margin_tri(U.tri[1], p, O.bo1, O.co1, d, cm, nm, &c1, &a1);   // wave-uniform
+        if (U.count == 2) margin_tri(U.tri[1], p, O.bo1, O.co1, d, cm, nm, &c1, &a1);
+#endif
         const float old = oc[k];
         const float c = fmaxf(c0, c1);
         oc[k] = fmaxf(old, c);
@@ -522,13 +583,23 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
     }
     if (!FORCE64 && do_closest && (rays & 8u)) {
         const RayPlane p = ray_plane(U, O.h, n32, INFINITY, INFINITY);
-        const Verdict v0 = classify_tri(U.tri[0], p, O.bo0, O.co0, n32);
-        bool c0 = v0.cand & !coplanar, c1 = false, a1 = false;
-        const bool a0 = v0.amb & !coplanar;
-        if (two) {
-            const Verdict v1 = classify_tri(U.tri[1], p, O.bo1, O.co1, n32);
+        bool c0, a0, c1 = false, a1 = false;
+        if (MARGIN && PT_QUAD) {   // the render loop's unit form (quad_m)
+            const QuadM m = quad_m(U, p, O, n32);
+            const Verdict v0 = verdict_m(m.m0, p), v1 = verdict_m(m.m1, p);
+            c0 = v0.cand & !coplanar;
+            a0 = v0.amb & !coplanar;
             c1 = v1.cand & !coplanar;
             a1 = v1.amb & !coplanar;
+        } else {
+            const Verdict v0 = classify_tri(U.tri[0], p, O.bo0, O.co0, n32);
+            c0 = v0.cand & !coplanar;
+            a0 = v0.amb & !coplanar;
+            if (two) {
+                const Verdict v1 = classify_tri(U.tri[1], p, O.bo1, O.co1, n32);
+                c1 = v1.cand & !coplanar;
+                a1 = v1.amb & !coplanar;
+            }
         }
         // both candidates of one unit cannot happen (a point certainly inside
         // one triangle is certainly outside its coplanar neighbour)
@@ -791,7 +862,7 @@ PT_HD UnitF bvh_unit(const SceneK& S, int i) {
     U.count = 1;
     U.obj = S.bvh_obj1 >= 0 ? S.bvh_obj1 : S.tri_obj[C.t];
     U.t[0] = U.t[1] = C.t;
-    U.pad = 0;
+    U.quad = 0;   // a single triangle
     U.tri[0] = C.tri;
     U.tri[1] = TriB{};
     return U;
@@ -1251,15 +1322,31 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         const int ogrp = S.tri_grp[tri];
         // RNG: the 16 slots of this bounce (4 Philox blocks in lockstep):
         // 0..11 light sampling, 12..14 the bounce, 15 Russian roulette
+        ShadowSet sh;
+#if PT_RNG_PERBLOCK
+        // one Philox block per light sample, drawn where it is used (fewer
+        // live registers than the four blocks in lockstep)
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < kLightSamples; ++k) {
+            uint32_t c[4];
+            rng_block(J.seed, J.pixel, sample, (uint32_t)b, (uint32_t)k, c);
+            shadow_setup_k<COUNT>(S, P, ld3(R.n), k, u_of(c[0]), u_of(c[1]), u_of(c[2]), u_of(c[3]),
+                                  &sh, sp);
+        }
+        sh.key2 = COUNT ? S.n_tri : S.n_obj;
+        sh.leak = S.n_obj - 1;
+        rng_block(J.seed, J.pixel, sample, (uint32_t)b, 3u, &w[12]);
+#else
         uint32_t w[16];
         rng_blocks4(J.seed, J.pixel, sample, (uint32_t)b, w);
-        ShadowSet sh;
         {
             double u12[12];
 #pragma unroll
             for (int i = 0; i < 12; ++i) u12[i] = u_of(w[i]);
             shadow_setup<COUNT>(S, P, ld3(R.n), u12, &sh, sp);
         }
+#endif
         // next ray (main.py:236-268): it does not depend on the colour
         double kf;
         const D3 nd = bounce(S, R, m, P, sp.get3(kSpNd), u_of(w[12]), u_of(w[13]), u_of(w[14]),
@@ -1283,7 +1370,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
             float oc[kLightSamples] = {-1.0f, -1.0f, -1.0f};
             for (int u = 0; u < S.n_obj_unit; ++u) {
                 const UnitF U = S.unit[u];
-                const OriginU O = origin_u(U, o32u);
+                const OriginU O = PT_QUAD ? origin_q(U, o32u) : origin_u(U, o32u);
 #ifdef PT_ABL_NOSHADOW   // timing ablation only (wrong results)
                 const bool do_shadow = false;
 #else

@@ -465,6 +465,48 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         return e + k * u * (g1 * Xb + fabs((double)(float)Cc)) * (1 + 4 * u) + 1e-30;
     };
     const double s = 1.25;   // safety factor over the first-order bounds below
+    // The barycentric forms of triangle t in frame f (0: "all", 1: "surface")
+    // with its vertices taken from vertex `rot` on (rot = 1: v2, v3, v1;
+    // 2: v3, v1, v2): beta = weight of the second, gamma of the third.  The
+    // inside test (every weight > 0) does not depend on the labelling.
+    // Returns false for a degenerate triangle (forms left zero).
+    auto tri_forms = [&](int t, int rot, int f, TriB* B, TriE* BE) {
+        *B = TriB{};
+        *BE = TriE{};
+        const D3 vv[3] = {tri_vertex(d, t, 0), tri_vertex(d, t, 1), tri_vertex(d, t, 2)};
+        const D3 Cf = f ? Cds : Cd;
+        const double Xf = f ? Xs : X;
+        const D3 w1 = vv[rot % 3] - Cf, w2 = vv[(rot + 1) % 3] - Cf, w3 = vv[(rot + 2) % 3] - Cf;
+        const D3 e1 = w2 - w1, e2 = w3 - w1, N = cross(e1, e2);
+        const double NN = dot(N, N);
+        if (!(NN > 0.0)) return false;
+        const D3 gb = cross(e2, N) * (1.0 / NN), gc = cross(N, e1) * (1.0 / NN);
+        const double cb = -dot(gb, w1), cc = -dot(gc, w1);
+        B->gb[0] = (float)gb.x; B->gb[1] = (float)gb.y; B->gb[2] = (float)gb.z; B->cb = (float)cb;
+        B->gc[0] = (float)gc.x; B->gc[1] = (float)gc.y; B->gc[2] = (float)gc.z; B->cc = (float)cc;
+        // Error bounds of the kernel's f32 forms (aff3 / lin3, pt_core.h):
+        // an affine form g.x + c at |x_i| <= X with g = f32(G), c = f32(C),
+        // x = f32(x_exact), evaluated as aff3's fma chain, errs by at most
+        //   sum_i |g_i - G_i| X + |c - C|           (coefficient rounding, exact)
+        // + u sum_i |g_i| X                        (input rounding)
+        // + k u (|g|_1 X + |c|)                    (one rounding per fma
+        //   whose product is nonzero: an fma with g_i = 0 returns its addend
+        //   exactly), k = nonzero coefficients;
+        // a direction form g.d (|d_i| <= 1, lin3) likewise with X = 1, c = 0.
+        // For a general plane this is <= 5u(|g|_1 X + |c|); for an
+        // axis-aligned one (walls: g one-hot and exact) ~2u(X + |c|), which
+        // decides most tests of lines grazing their edges in f32.  The
+        // safety factor s covers second-order terms and the reference's own
+        // f64 rounding (~1e-16 relative).
+        const double gbd[3] = {gb.x, gb.y, gb.z}, gcd[3] = {gc.x, gc.y, gc.z};
+        const double gb1 = l1(B->gb[0], B->gb[1], B->gb[2]) * (1 + 4 * u);
+        const double gc1 = l1(B->gc[0], B->gc[1], B->gc[2]) * (1 + 4 * u);
+        // x2: one bound for beta, gamma (error <= del/2) and alpha (<= del)
+        BE->eo = f32_up(2 * (s * std::max(aff_err(gbd, cb, Xf), aff_err(gcd, cc, Xf)) + 8 * u));
+        BE->ed = f32_up(2 * s * std::max(aff_err(gbd, 0.0, 1.0), aff_err(gcd, 0.0, 1.0)));
+        BE->g = f32_up(2 * std::max(gb1, gc1) * (1 + 1e-3));
+        return true;
+    };
     for (int t = 0; t < T; ++t) {
         const D3 v1 = tri_vertex(d, t, 0), v2 = tri_vertex(d, t, 1), v3 = tri_vertex(d, t, 2);
         TriD& E = H->trid[t];
@@ -488,49 +530,23 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         for (int f = 0; f < 2; ++f) {
             const D3 Cf = f ? Cds : Cd;
             const double Xf = f ? Xs : X;
-            const D3 w1 = v1 - Cf, w2 = v2 - Cf, w3 = v3 - Cf;
-            const D3 e1 = w2 - w1, e2 = w3 - w1, N = cross(e1, e2);
-            const double NN = dot(N, N);
+            const D3 w1 = v1 - Cf;
             PlaneD& P = f ? pls[t] : pl[t];
-            TriB& B = f ? tbs[t] : tb[t];
-            B = TriB{};
-            TriE& BE = f ? tes[t] : te[t];
-            BE = TriE{};
-            P.ok = (cn > 0.0) && (NN > 0.0) && isfinite(cn);
-            if (!P.ok) continue;   // degenerate: the reference's NaN normal never hits
-            const D3 gb = cross(e2, N) * (1.0 / NN), gc = cross(N, e1) * (1.0 / NN);
-            const double cb = -dot(gb, w1), cc = -dot(gc, w1);
+            const bool formed = tri_forms(t, 0, f, f ? &tbs[t] : &tb[t], f ? &tes[t] : &te[t]);
+            P.ok = (cn > 0.0) && formed && isfinite(cn);
+            if (!P.ok) {   // degenerate: the reference's NaN normal never hits
+                (f ? tbs[t] : tb[t]) = TriB{};
+                (f ? tes[t] : te[t]) = TriE{};
+                continue;
+            }
             const double chn = -(E.vp[0] * w1.x + E.vp[1] * w1.y + E.vp[2] * w1.z);
             for (int i = 0; i < 3; ++i) P.n[i] = E.vp[i];
             P.cn = chn;
-            B.gb[0] = (float)gb.x; B.gb[1] = (float)gb.y; B.gb[2] = (float)gb.z; B.cb = (float)cb;
-            B.gc[0] = (float)gc.x; B.gc[1] = (float)gc.y; B.gc[2] = (float)gc.z; B.cc = (float)cc;
-            // Error bounds of the kernel's f32 forms (aff3 / lin3, pt_core.h):
-            // an affine form g.x + c at |x_i| <= X with g = f32(G), c = f32(C),
-            // x = f32(x_exact), evaluated as aff3's fma chain, errs by at most
-            //   sum_i |g_i - G_i| X + |c - C|           (coefficient rounding, exact)
-            // + u sum_i |g_i| X                        (input rounding)
-            // + k u (|g|_1 X + |c|)                    (one rounding per fma
-            //   whose product is nonzero: an fma with g_i = 0 returns its addend
-            //   exactly), k = nonzero coefficients;
-            // a direction form g.d (|d_i| <= 1, lin3) likewise with X = 1, c = 0.
-            // For a general plane this is <= 5u(|g|_1 X + |c|); for an
-            // axis-aligned one (walls: g one-hot and exact) ~2u(X + |c|), which
-            // decides most tests of lines grazing their edges in f32.  The
-            // safety factor s covers second-order terms and the reference's own
-            // f64 rounding (~1e-16 relative).
             const double nd3[3] = {E.vp[0], E.vp[1], E.vp[2]};
-            const double gbd[3] = {gb.x, gb.y, gb.z}, gcd[3] = {gc.x, gc.y, gc.z};
             const double n1 = l1((float)P.n[0], (float)P.n[1], (float)P.n[2]) * (1 + 4 * u);
-            const double gb1 = l1(B.gb[0], B.gb[1], B.gb[2]) * (1 + 4 * u);
-            const double gc1 = l1(B.gc[0], B.gc[1], B.gc[2]) * (1 + 4 * u);
             P.eh = s * aff_err(nd3, chn, Xf);
             // q's own error, plus 8u n1 >= 8u|q| covering the rounding of 1/q and t
             P.eq = s * aff_err(nd3, 0.0, 1.0) + 8 * u * n1;
-            // x2: one bound for beta, gamma (error <= del/2) and alpha (<= del)
-            BE.eo = f32_up(2 * (s * std::max(aff_err(gbd, cb, Xf), aff_err(gcd, cc, Xf)) + 8 * u));
-            BE.ed = f32_up(2 * s * std::max(aff_err(gbd, 0.0, 1.0), aff_err(gcd, 0.0, 1.0)));
-            BE.g = f32_up(2 * std::max(gb1, gc1) * (1 + 1e-3));
         }
     }
     // coplanar groups: triangle t joins the group of an earlier
@@ -590,8 +606,41 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     H->unit.clear();
     H->unit_eye.clear();
     H->bunit.clear();
+    // Parallelogram pairs ("quads", e.g. the reference's rectangles split
+    // along a diagonal): triangles t, t + 1 share two vertices i1, i2 (the
+    // diagonal), t's third vertex k and t + 1's third vertex D satisfy
+    // D = i1 + i2 - k.  Then t + 1's weights at (i1, i2, D) are
+    // (1 - l_i2, 1 - l_i1, -l_k) in t's weights l, so with t's forms taken
+    // from vertex rot on (tri_forms: the order i2, k, i1, so alpha = l_i2,
+    // beta = l_k, gamma = l_i1) they are (beta + gamma, 1 - gamma, -beta): the
+    // render loop tests both members from one pair of forms (pt_path.h
+    // quad_m).  Returns rot, or -1 when the
+    // pair is no parallelogram; *dev = |i1 + i2 - k - D|_1 (f64).
+    auto quad_rot = [&](int t, double* dev) {
+        D3 a[3], b[3];
+        for (int v = 0; v < 3; ++v) a[v] = tri_vertex(d, t, v), b[v] = tri_vertex(d, t + 1, v);
+        auto same = [](D3 p, D3 q) { return p.x == q.x && p.y == q.y && p.z == q.z; };
+        int k = -1, ns = 0;
+        bool used[3] = {false, false, false};
+        for (int i = 0; i < 3; ++i) {
+            bool sh = false;
+            for (int j = 0; j < 3 && !sh; ++j)
+                if (!used[j] && same(a[i], b[j])) { used[j] = sh = true; ++ns; }
+            if (!sh) k = i;
+        }
+        if (ns != 2 || k < 0) return -1;
+        int jd = 0;
+        while (used[jd]) ++jd;
+        const D3 i1 = a[(k + 1) % 3], i2 = a[(k + 2) % 3];
+        const D3 e = ((i1 + i2) - a[k]) - b[jd];
+        double sc = 0.0;
+        for (const D3& q : {i1, i2, a[k], b[jd]}) sc = std::max(sc, l1(q.x, q.y, q.z));
+        *dev = l1(e.x, e.y, e.z) + 8e-16 * sc;   // + the rounding of the check itself
+        if (!(*dev <= 1e-12 * (sc + 1.0))) return -1;
+        return (k + 2) % 3;   // rotated order (v[rot], v[rot+1], v[rot+2]): v[k] second
+    };
     // one unit record in frame f (0: all, 1: surface) for triangles t (, t + 1)
-    auto make_unit = [&](int t, bool pair, int f) {
+    auto make_unit = [&](int t, bool pair, int f, int rot = -1, double dev = 0.0) {
         const std::vector<PlaneD>& PL = f ? pls : pl;
         const std::vector<TriB>& TB = f ? tbs : tb;
         const std::vector<TriE>& TE = f ? tes : te;
@@ -604,6 +653,7 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         U.tri[1] = pair ? TB[t + 1] : TriB{};
         U.t[0] = t;
         U.t[1] = pair ? t + 1 : t;
+        U.quad = pair ? -1 : 0;   // a pair that is no parallelogram / a single
         U.eo = TE[t].eo;
         U.ed = TE[t].ed;
         U.g = TE[t].g;
@@ -622,6 +672,22 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
                 U.ed = std::max(TE[t].ed, TE[t + 1].ed);
                 U.g = std::max(TE[t].g, TE[t + 1].g);
             }
+            if (rot >= 0) {   // a quad: the first member's forms from vertex rot on
+                TriB B0;
+                TriE E0;
+                tri_forms(t, rot, f, &B0, &E0);
+                U.tri[0] = B0;
+                U.quad = 1;
+                // + the quad relation's own mismatch: moving the second
+                // member's vertex D by dev changes its weights at x by at most
+                // dev |grad l|_1 |l_D(x)| <= dev (g / 2) (3 (g / 2) X + 1) in
+                // the frame's box (x2: eo's convention)
+                const double gm = std::max(E0.g, TE[t + 1].g), Xf = f ? Xs : X;
+                U.eo = f32_up(std::max((double)E0.eo, (double)TE[t + 1].eo) + 2e-9 +
+                              dev * gm * (1.5 * gm * Xf + 1.0));
+                U.ed = std::max(E0.ed, TE[t + 1].ed);
+                U.g = std::max(E0.g, TE[t + 1].g);
+            }
             for (int i = 0; i < 3; ++i) U.n[i] = (float)P.n[i];
             U.cn = (float)P.cn;
             U.eh = f32_up(eh);
@@ -633,14 +699,16 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     for (int part = 0; part < 2; ++part) {
         const int t_begin = part == 0 ? 0 : d->n_obj_tri, t_end = part == 0 ? d->n_obj_tri : T;
         for (int t = t_begin; t < t_end;) {
-            const bool pair = (t + 1 < t_end) && pl[t].ok && pl[t + 1].ok &&
-                              H->tri_grp[t] >= 0 && H->tri_grp[t + 1] == H->tri_grp[t] &&
-                              d->tri_obj[t + 1] == d->tri_obj[t];
+            bool pair = (t + 1 < t_end) && pl[t].ok && pl[t + 1].ok &&
+                        H->tri_grp[t] >= 0 && H->tri_grp[t + 1] == H->tri_grp[t] &&
+                        d->tri_obj[t + 1] == d->tri_obj[t];
             if (in_bvh(t)) {
                 H->bunit.push_back(make_unit(t, pair, 0));
             } else {
-                H->unit.push_back(make_unit(t, pair, 1));
-                H->unit_eye.push_back(make_unit(t, pair, 0));
+                double dev = 0.0;
+                const int rot = pair ? quad_rot(t, &dev) : -1;
+                H->unit.push_back(make_unit(t, pair, 1, rot, dev));
+                H->unit_eye.push_back(make_unit(t, pair, 0, rot, dev));
             }
             t += pair ? 2 : 1;
         }

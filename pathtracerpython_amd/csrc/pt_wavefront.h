@@ -177,7 +177,7 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
         float oc[kLightSamples] = {-1.0f, -1.0f, -1.0f};
         for (int u = 0; u < S.n_obj_unit; ++u) {
             const UnitF U = S.unit[u];
-            const OriginU O = origin_u(U, o32u);
+            const OriginU O = PT_QUAD ? origin_q(U, o32u) : origin_u(U, o32u);
             const bool do_shadow = PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));
             fused_unit<false, false, true>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
                                            &ca, sp, nullptr, 15u, oc);

@@ -318,6 +318,28 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
                 if (ms != kAmb && (ms == kCand) != ref_s) ++wrong;
                 if (ms != st && !(st == kMiss && ms == kAmb)) ++mdiff;
             }
+            if (uni) {   // the render loop's unit form (quad_m): both members' tests
+                float cm, nm;
+                margin_plane(U, ps, hlo, hhi, INFINITY, &cm, &nm);
+                const OriginU Oq = origin_q(U, at_eye ? o32 : o32s);
+                const QuadM qs = quad_m(U, ps, Oq, d32), qc = quad_m(U, pc, Oq, d32);
+                for (int i = 0; i < 2; ++i) {
+                    D3 Q; double sqd;
+                    const bool h = i < U.count && eval64(H.trid[U.t[i]], o, dn, &Q, &sqd);
+                    float mc, ma;
+                    margin_m(i ? qs.m1 : qs.m0, ps, cm, nm, &mc, &ma);
+                    const int ms = mc > 0.0f ? kCand : (ma >= 0.0f ? kAmb : kMiss);
+                    const bool ref_s = h && !(sqd < kZero) && sqd < lim;
+                    ++tests;
+                    if (ms == kAmb) ++amb;
+                    else if ((ms == kCand) != ref_s) ++wrong;
+                    const int vc = verdict_code(verdict_m(i ? qc.m1 : qc.m0, pc));
+                    const bool ref_c = h && sqd > kZero;
+                    ++tests;
+                    if (vc == kAmb) ++amb;
+                    else if ((vc == kCand) != ref_c) ++wrong;
+                }
+            }
         }
     }
     out[0] = wrong; out[1] = amb; out[2] = tests; out[3] = cand; out[4] = mdiff;
