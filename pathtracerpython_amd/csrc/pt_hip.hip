@@ -935,8 +935,14 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
         // quarter of the rows at 2x / 4x / 8x lanes all land within 6.49-6.54.
         // A pixel's lanes depend only on (iy, W, H, spp), so band renders
         // still assemble bit for bit.
-        constexpr int kTailFrac = 16;
-        constexpr uint32_t kTailMul = 3;   // log2 of the lane multiplier
+#ifndef PT_TAIL_FRAC
+#define PT_TAIL_FRAC 16
+#endif
+#ifndef PT_TAIL_MUL
+#define PT_TAIL_MUL 3
+#endif
+        constexpr int kTailFrac = PT_TAIL_FRAC;
+        constexpr uint32_t kTailMul = PT_TAIL_MUL;   // log2 of the lane multiplier
         uint32_t cap = 64;
         while (cap > 1 && (int32_t)cap > p->spp) cap >>= 1;
         const uint32_t tl = std::min(R.split_log2 + kTailMul, (uint32_t)__builtin_ctz(cap));

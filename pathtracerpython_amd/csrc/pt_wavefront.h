@@ -147,15 +147,28 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
     const TriS R = S.tris[tri];
     const Mat& m = S.mat[obj];
     const int ogrp = S.tri_grp[tri];
-    uint32_t w[16];
-    rng_blocks4(J.seed, J.pixel, sample, (uint32_t)b, w);
     ShadowSet sh;
+    uint32_t w[16];
+#if PT_RNG_PERBLOCK   // as render_lane: one Philox block per light sample, where it is used
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        uint32_t c[4];
+        rng_block(J.seed, J.pixel, sample, (uint32_t)b, (uint32_t)k, c);
+        shadow_setup_k<false>(S, P, ld3(R.n), k, u_of(c[0]), u_of(c[1]), u_of(c[2]), u_of(c[3]),
+                              &sh, sp);
+    }
+    sh.key2 = S.n_obj;
+    sh.leak = S.n_obj - 1;
+    rng_block(J.seed, J.pixel, sample, (uint32_t)b, 3u, &w[12]);
+#else
+    rng_blocks4(J.seed, J.pixel, sample, (uint32_t)b, w);
     {
         double u12[12];
 #pragma unroll
         for (int i = 0; i < 12; ++i) u12[i] = u_of(w[i]);
         shadow_setup<false>(S, P, ld3(R.n), u12, &sh, sp);
     }
+#endif
     double kf;
     const D3 nd = bounce(S, R, m, P, sp.get3(kSpNd), u_of(w[12]), u_of(w[13]), u_of(w[14]), &kf);
     const double kn = W->k * kf;
