@@ -346,7 +346,7 @@ def cpu_baseline(oracle, packed, W, H, SPP, B, config):
     t1 = time.perf_counter()
     oracle.render(packed, W, H, SPP, B, SEED, pixels=pix, threads=threads)
     cdt = time.perf_counter() - t1
-    return {"value": round(len(pix) * SPP / cdt / 1e6, 4), "unit": "Mpath-samples/s",
+    return {"value": float("%.4g" % (len(pix) * SPP / cdt / 1e6)), "unit": "Mpath-samples/s",
             "cores": threads, "kind": "port",
             "host_cpus_visible": len(os.sched_getaffinity(0)),
             "sample": f"oracle/pt_oracle.c (f64 C restatement of main.py:186-280) on {sample}: "
