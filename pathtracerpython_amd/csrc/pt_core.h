@@ -274,7 +274,14 @@ PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t 
 // One Philox4x32-10 block: slots 4 blk .. 4 blk + 3 of (pixel, sample, bounce)
 PT_HD void rng_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t blk,
                      uint32_t c[4]) {
+#if PT_RNG_OPQ & 1
+    pixel = pt_opaque(pixel);
+#endif
+#if PT_RNG_OPQ & 2
+    uint32_t k0 = pt_opaque_s((uint32_t)seed), k1 = pt_opaque_s((uint32_t)(seed >> 32));
+#else
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#endif
     c[0] = pixel; c[1] = sample; c[2] = bounce; c[3] = blk;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
