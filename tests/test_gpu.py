@@ -10,7 +10,7 @@ determinism) cover the whole image."""
 import numpy as np
 import pytest
 
-from conftest import golden_renders, multi_mesh_scene, random_scene
+from conftest import golden_renders, multi_mesh_scene, quad_scene, random_scene
 from oracle import oracle
 from pathtracerpython_amd import _native
 from pathtracerpython_amd.pack import pack_scene
@@ -172,6 +172,20 @@ def test_random_mesh_scene(tmp_path):
     assert np.abs(to_list_order(fb) - ref).max() <= TOL
     with Renderer(sc) as r:   # wavefront (default for BVH scenes) == single kernel
         assert np.array_equal(fb, r.render(48, 48, 4, 5, 8, out_f64=True, megakernel=True))
+
+
+@pytest.mark.parametrize("seed", [3, 8])
+def test_quad_units_scene(tmp_path, seed):
+    """Parallelogram units in every vertex labelling, skewed coplanar pairs
+    and single triangles (the render loop's unit form, pt_path.h quad_m):
+    hybrid == forced f64 bit for bit, and the oracle to rounding."""
+    sc = quad_scene(tmp_path, seed)
+    pk = pack_scene(sc)
+    with Renderer(sc) as r:
+        fb = r.render(64, 64, 8, 5, seed, out_f64=True)
+        assert np.array_equal(fb, r.render(64, 64, 8, 5, seed, out_f64=True, force_f64=True))
+    ref, _ = oracle.render(pk, 64, 64, 8, 5, seed)
+    assert np.abs(to_list_order(fb) - ref).max() <= TOL
 
 
 @pytest.mark.parametrize("seed", [3, 4])
