@@ -521,4 +521,45 @@ void hc_rng4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce, ui
     rng_blocks4(seed, pixel, sample, bounce, out);
 }
 
+// Bounce-loop iterations of every lane of a single-kernel launch with `split`
+// lanes per pixel (lane c of a pixel runs samples c, c + split, ...), the
+// pixels of the selected rows in launch order: out[pixel * split + c] (dev
+// tool: the lane-utilisation bound of a wave is sum / (64 max) over its 64).
+int hc_lane_iters(const pt_scene_desc* d, const pt_render_params* p, int32_t split,
+                  int32_t* out) {
+    HostScene H;
+    if (!prepare_scene(d, &H).empty()) return -1;
+    bind_host(&H);
+    int32_t first, rows;
+    if (!band_layout(p, &first, &rows)) return -2;
+    double spill_mem[kSpillSlots];
+    const Spill sp{spill_mem, 1};
+    const D3 eye = ld3(H.k.eye);
+    for (int r = 0; r < rows; ++r) {
+        const int iy = first + r * p->row_step;
+        for (int ix = 0; ix < p->width; ++ix) {
+            const double x = linspace_at(H.k.ortho[0], H.k.ortho[2], p->width, ix);
+            const double y = linspace_at(H.k.ortho[1], H.k.ortho[3], p->height, iy);
+            const D3 d0 = d3(x - eye.x, y - eye.y, 0.0 - eye.z);
+            Counters c0 = {};
+            D3 P0 = d3(0, 0, 0);
+            const int tri0 = p->bounces > 0 ? closest<false, false>(H.k, eye, d0, -1, sp, &P0, &c0, true) : -1;
+            for (int c = 0; c < split; ++c) {
+                LaneJob J;
+                J.seed = p->seed;
+                J.pixel = (uint32_t)ix * (uint32_t)p->height + (uint32_t)iy;
+                J.sample0 = p->sample_begin + c;
+                J.sample_stride = split;
+                J.n_samples = c < p->spp ? (p->spp - c + split - 1) / split : 0;
+                J.bounces = p->bounces;
+                J.rr_depth = (p->flags & PT_FLAG_RR) ? p->rr_depth : -1;
+                Counters cnt = {};
+                render_lane<false, true>(H.k, J, d0, tri0, P0, sp, &cnt);
+                out[((size_t)r * p->width + ix) * split + c] = (int32_t)cnt.shading_points;
+            }
+        }
+    }
+    return 0;
+}
+
 }  // extern "C"
