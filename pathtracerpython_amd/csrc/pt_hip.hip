@@ -743,11 +743,13 @@ static uint32_t choose_split(uint64_t image_pixels, int32_t spp, bool bvh) {
 // 130 / 174 ms; grids of 1 / 2 / 3 / 4 / 16 blocks per CU -> 271 / 174 / 169
 // / 178 / 188 ms.  Compile-time (-D) so tuning builds can sweep them; the
 // shipped library has no run-time knobs.
+// Round 2 re-sweep (512^2 x 64 spp render, both walks): 16 / 24 / 32 / 40 /
+// 48 -> 114.3 / 110.5 / 108.0 / 107.8 / 109.5 ms.
 #ifndef PT_WF_THR_SHADOW
-#define PT_WF_THR_SHADOW 24
+#define PT_WF_THR_SHADOW 32
 #endif
 #ifndef PT_WF_THR_CLOSEST
-#define PT_WF_THR_CLOSEST 24
+#define PT_WF_THR_CLOSEST 32
 #endif
 #ifndef PT_WF_SHADOW_BLOCKS_PER_CU
 #define PT_WF_SHADOW_BLOCKS_PER_CU 4
