@@ -186,7 +186,8 @@ __global__ __launch_bounds__(256, PT_RENDER_WAVES) void k_render(SceneK S, Rende
 
 // ------------------------------------------------- wavefront (BVH scenes) --
 // pt_wavefront.h.  Queue counters: [0] shadow count, [1] shadow head,
-// [2] closest count, [3] closest head; lists[0..slots) shadow, then closest.
+// [2] closest count, [3] closest head; lists[0..3 slots) the shadow rays
+// ((slot << 2) | ray), then [3 slots, 4 slots) closest.
 // A walk kernel gets its list and its [count, head] pair.
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -203,6 +204,27 @@ __device__ __forceinline__ void wf_append(bool want, int32_t* counter, int32_t* 
     if (lane_id() == leader) base = atomicAdd(counter, (int32_t)__popcll(m));
     base = __shfl(base, (int)leader);
     if (want) list[base + (int32_t)lanes_below(m)] = v;
+}
+// the same for the shadow rays (bits 0..2 of want): one atomic per wave for
+// all three (a single counter takes every wave's appends), entries
+// (slot << 2) | ray, ray-major within the wave's block
+__device__ __forceinline__ void wf_append3(uint32_t want, int32_t* counter, int32_t* list, int32_t slot) {
+    uint64_t m[kLightSamples];
+    int32_t n = 0, off[kLightSamples];
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        m[k] = __ballot(((want >> k) & 1u) != 0);
+        off[k] = n;
+        n += (int32_t)__popcll(m[k]);
+    }
+    if (n == 0) return;
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u;
+    int32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(counter, n);
+    base = __shfl(base, (int)leader);
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k)
+        if ((want >> k) & 1u) list[base + off[k] + (int32_t)lanes_below(m[k])] = wf_shadow_entry(slot, k);
 }
 // Next list positions for the lanes that need one.  A wave claims a chunk of
 // kWfChunk consecutive positions with one atomic on the list head and hands
@@ -252,8 +274,8 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
     } else if (j.valid && W[tid].state != kWfDone) {
         want = wf_shade(S, j.J, j.d0, &W[tid], &SQ[tid], &CQ[tid]);
     }
-    wf_append((want & kWfWantShadow) != 0, &counters[0], lists, (int32_t)tid);
-    wf_append((want & kWfWantClosest) != 0, &counters[2], lists + slots, (int32_t)tid);
+    wf_append3(want, &counters[0], lists, (int32_t)tid);   // one shadow walk per open ray
+    wf_append((want & kWfWantClosest) != 0, &counters[2], lists + 3 * (size_t)slots, (int32_t)tid);
 }
 
 // Persistent walk kernels over the 4-wide quantised BVH (QNode): a
@@ -270,8 +292,8 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
 // the rest in global memory.  Smaller shared-memory stacks let more
 // work-groups share a CU (the walks wait on dependent node loads: occupancy
 // is their latency hiding).
-#ifndef PT_SHADOW_WAVES
-#define PT_SHADOW_WAVES 1
+#ifndef PT_SHADOW_WAVES   // one-ray shadow walk: 5 waves/SIMD (90 VGPRs, no spills; 6: spills)
+#define PT_SHADOW_WAVES 5
 #endif
 #ifndef PT_CLOSEST_WAVES
 #define PT_CLOSEST_WAVES 5
@@ -300,6 +322,8 @@ __device__ __forceinline__ void flush_walk_counts(uint32_t q, uint32_t nodes, ui
 }
 __device__ __forceinline__ uint32_t leaf_units(int ref) { return (uint32_t)(~ref) & 7u; }
 
+// The shadow walks: one work-item per open shadow ray (list entries
+// (slot << 2) | ray, pt_path.h "one-ray shadow walks").
 template <bool UC, bool COUNT>
 __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, WfPath* __restrict__ W,
                                                    WfShadowQ* __restrict__ SQ,
@@ -316,23 +340,23 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
     __shared__ int stack[kWalkStackLds][256];
     const int lanes = (int)gridDim.x * 256, gl = (int)(blockIdx.x * 256u + threadIdx.x);
     const ShadowStack K{&stack[0][threadIdx.x], 256, ovf + gl, lanes, kWalkStackLds};
-    ShadowSet sh;
-    ShadowTrav T;
+    Shadow1 r;
+    ShadowTrav1 T;
     T.ref = kNoRef;
-    int pl = kNoRef, pl2 = kNoRef;   // postponed leaves and their rays
-    uint32_t plr = 0, plr2 = 0;
+    int pl = kNoRef, pl2 = kNoRef;   // postponed leaves
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
             const int32_t i = wf_fetch(need, &counters[1], cb, ce);
             if (need) {
                 if (i < count) {
-                    slot = list[i];
+                    const int32_t e = list[i];
+                    slot = e >> 2;
                     if (COUNT) ++c_q;
                     F3 o32;
                     int ogrp;
-                    wf_get_shadow(S, SQ[slot], &o32, &ogrp, &sh);
-                    strav_init<false>(T, S, o32, ogrp, &sh, S.qroot);
+                    wf_get_shadow1(SQ[slot], e & 3, &o32, &ogrp, &r);
+                    s1_init(T, S, o32, ogrp, r, S.qroot);
                 } else {
                     exhausted = true;
                 }
@@ -344,9 +368,9 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
         // leaves per lane and fewer lanes idle in this loop.
         while (true) {
             if (slot >= 0 && T.ref <= -2 && pl2 == kNoRef) {
-                if (pl == kNoRef) { pl = T.ref; plr = T.rays; }
-                else { pl2 = T.ref; plr2 = T.rays; }
-                T.ref = strav_pop<false>(T, K, S, &sh);
+                if (pl == kNoRef) pl = T.ref;
+                else pl2 = T.ref;
+                T.ref = s1_pop(T, K, S, r);
             }
             const bool desc = slot >= 0 && T.ref >= 0;
             const int32_t nd = (int32_t)__popcll(__ballot(desc));
@@ -354,7 +378,7 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
             if (nd == 0 || (nd <= thr && __any(slot >= 0 && (pl != kNoRef || T.ref <= -2)))) break;
             if (desc) {
                 if (COUNT) ++c_nodes;
-                strav_qnode<false>(T, K, S, &sh);
+                s1_qnode(T, K, S, r);
             }
         }
         if (slot >= 0) {
@@ -362,17 +386,18 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
             if (COUNT)
                 c_units += (pl != kNoRef ? leaf_units(pl) : 0u) + (pl2 != kNoRef ? leaf_units(pl2) : 0u) +
                            (T.ref <= -2 ? leaf_units(T.ref) : 0u);
-            if (pl != kNoRef) strav_units<false, UC>(T, S, &sh, sp, nullptr, pl, plr);
-            if (pl2 != kNoRef) strav_units<false, UC>(T, S, &sh, sp, nullptr, pl2, plr2);
+            if (pl != kNoRef) s1_units<UC>(T, S, &r, sp, pl);
+            if (pl2 != kNoRef) s1_units<UC>(T, S, &r, sp, pl2);
             pl = pl2 = kNoRef;
-            if (T.ref <= -2) strav_leaf<false, UC>(T, K, S, &sh, sp, nullptr);
+            if (T.ref <= -2) {
+                s1_units<UC>(T, S, &r, sp, T.ref);
+                T.ref = s1_pop(T, K, S, r);
+            }
+            // a ray closed meanwhile drops what is left (entries, a node)
+            if (!shadow1_open(S, r)) T.ref = kNoRef;
         }
         if (slot >= 0 && T.ref == kNoRef) {
-            int occ = 0;
-#pragma unroll
-            for (int k = 0; k < kLightSamples; ++k) occ |= sh.occ[k] ? 1 << k : 0;
-            SQ[slot].occ = occ;
-            SQ[slot].leak = sh.leak;
+            wf_put_shadow1(&SQ[slot], r);
             slot = -1;
         }
     }
@@ -744,15 +769,16 @@ static uint32_t choose_split(uint64_t image_pixels, int32_t spp, bool bvh) {
 // / 178 / 188 ms.  Compile-time (-D) so tuning builds can sweep them; the
 // shipped library has no run-time knobs.
 // Round 2 re-sweep (512^2 x 64 spp render, both walks): 16 / 24 / 32 / 40 /
-// 48 -> 114.3 / 110.5 / 108.0 / 107.8 / 109.5 ms.
+// 48 -> 114.3 / 110.5 / 108.0 / 107.8 / 109.5 ms; the one-ray shadow walk's
+// threshold 16 / 24 / 32 / 40 / 48 -> 100.7 / 98.8 / 97.4 / 96.9 / 96.9 ms.
 #ifndef PT_WF_THR_SHADOW
-#define PT_WF_THR_SHADOW 32
+#define PT_WF_THR_SHADOW 40
 #endif
 #ifndef PT_WF_THR_CLOSEST
 #define PT_WF_THR_CLOSEST 32
 #endif
 #ifndef PT_WF_SHADOW_BLOCKS_PER_CU
-#define PT_WF_SHADOW_BLOCKS_PER_CU 4
+#define PT_WF_SHADOW_BLOCKS_PER_CU 5
 #endif
 #ifndef PT_WF_CLOSEST_BLOCKS_PER_CU
 #define PT_WF_CLOSEST_BLOCKS_PER_CU 5
@@ -770,7 +796,7 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
                             uint32_t flags, pt_stats* stats) {
     const size_t slots = (size_t)grid.x * 256;
     const size_t sz_w = slots * sizeof(WfPath), sz_s = slots * sizeof(WfShadowQ),
-                 sz_c = slots * sizeof(WfClosestQ), sz_l = 2 * slots * sizeof(int32_t);
+                 sz_c = slots * sizeof(WfClosestQ), sz_l = 4 * slots * sizeof(int32_t);
     const unsigned sh_blocks =
         std::max(1u, std::min<unsigned>(grid.x, (unsigned)PT_WF_SHADOW_BLOCKS_PER_CU * (unsigned)s->n_cu));
     const unsigned cl_blocks =
@@ -823,7 +849,7 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
         return times ? hipEventRecord(s->prof_ev[(size_t)step * 6 + k * 2 + end], on) : hipSuccess;
     };
     auto closest_walk = [&](hipStream_t on) {
-        const int32_t* l = lists + slots;
+        const int32_t* l = lists + 3 * slots;
         if (s->dev.bunitc) {
             if (wcount) hipLaunchKernelGGL((k_wf_closest<true, true>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd);
             else hipLaunchKernelGGL((k_wf_closest<true, false>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd);
@@ -973,10 +999,12 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     const bool f64 = (p->flags & PT_FLAG_FORCE_F64) != 0;
     // BVH scenes render through the wavefront kernels unless the caller asks
     // for the single kernel (and for counting / forced-f64 launches, which
-    // only the single kernel implements)
+    // only the single kernel implements; and for launches of 2^29 or more
+    // path slots, beyond the shadow lists' (slot << 2) | ray entries — the
+    // single kernel's framebuffer is the same bit for bit)
     const bool wavefront = s->dev.n_bnode > 0 && !count && !f64 &&
                            !(p->flags & PT_FLAG_MEGAKERNEL) && s->dev.n_qnode > 0 &&
-                           s->dev.qstack <= kWalkStack;
+                           s->dev.qstack <= kWalkStack && (uint64_t)grid.x * 256u < ((uint64_t)1 << 29);
     if (wavefront) return render_wavefront(s, R, grid, out_dev, st, p->flags, stats);
     if (count) HIPCHK(hipMemsetAsync(s->stats, 0, sizeof(StatsDev), st));
     HIPCHK(hipEventRecord(s->ev0, st));

@@ -40,15 +40,17 @@ struct alignas(16) WfPath {
 };
 static_assert(sizeof(WfPath) == 256, "WfPath is 256 B");
 
-// shadow walk: in = the state after the uniform units, out = the final state
+// shadow walks: in = the state after the uniform units, out = the final
+// state.  The one-ray walks of a query write disjoint fields: ray 0 / 1 its
+// wocc entry, ray 2 bit 2 of occ and leak.
 struct alignas(16) WfShadowQ {
     float o[3];
     int32_t ogrp;
     float d[kLightSamples][3];
     float hlo[kLightSamples], hhi[kLightSamples];
-    int32_t occ;              // bit k: shadow ray k occluded
+    int32_t occ;              // bit k: shadow ray k occluded (the uniform units; ray 2's walk)
     int32_t key2, leak;
-    int32_t pad[2];
+    int32_t wocc[2];          // rays 0, 1: occluded by the BVH (their walks)
 };
 static_assert(sizeof(WfShadowQ) == 96, "WfShadowQ is 96 B");
 
@@ -77,6 +79,7 @@ PT_HD void wf_put_shadow(WfShadowQ* q, F3 o32, int ogrp, const ShadowSet& sh) {
     q->occ = occ;
     q->key2 = sh.key2;
     q->leak = sh.leak;
+    q->wocc[0] = q->wocc[1] = 0;
 }
 // the walk's view of a query (count-mode fields unused: the wavefront path
 // does not count)
@@ -95,6 +98,30 @@ PT_HD void wf_get_shadow(const SceneK& S, const WfShadowQ& q, F3* o32, int* ogrp
     sh->key2 = q.key2;
     sh->leak = q.leak;
 }
+// a one-ray walk's view of shadow ray k of a query
+PT_HD void wf_get_shadow1(const WfShadowQ& q, int k, F3* o32, int* ogrp, Shadow1* r) {
+    *o32 = F3{q.o[0], q.o[1], q.o[2]};
+    *ogrp = q.ogrp;
+    r->d32 = F3{q.d[k][0], q.d[k][1], q.d[k][2]};
+    r->hlo = q.hlo[k];
+    r->hhi = q.hhi[k];
+    r->k = k;
+    r->occ = false;   // (only open rays are walked)
+    r->key2 = q.key2;
+    r->leak = q.leak;
+}
+// its result into the query record (fields of ray k only)
+PT_HD void wf_put_shadow1(WfShadowQ* q, const Shadow1& r) {
+    if (r.k < kLightSamples - 1) {
+        q->wocc[r.k] = r.occ ? 1 : 0;
+    } else {
+        if (r.occ) q->occ |= 1 << r.k;
+        q->leak = r.leak;
+    }
+}
+// list entries of the shadow walks: (slot << 2) | ray
+PT_HD int32_t wf_shadow_entry(int32_t slot, int k) { return (slot << 2) | k; }
+
 PT_HD void wf_put_closest(WfClosestQ* q, F3 o32, int ogrp, F3 d32, const ClosestAcc& c) {
     q->o[0] = o32.x; q->o[1] = o32.y; q->o[2] = o32.z;
     q->ogrp = ogrp;
@@ -108,8 +135,9 @@ PT_HD ClosestAcc wf_get_acc(const WfClosestQ& q) {
     return c;
 }
 
-// What a shade step asks for next (bit 0: a shadow walk, bit 1: a closest walk)
-enum : uint32_t { kWfWantShadow = 1u, kWfWantClosest = 2u };
+// What a shade step asks for next (bit k < 3: a walk of shadow ray k, bit 3:
+// a closest walk)
+enum : uint32_t { kWfWantShadow = 7u, kWfWantClosest = 8u };
 
 // Start the slot (shade step 0): the primary ray's uniform part, as closest()
 // does for it in k_render; the BVH part is a closest query.
@@ -207,7 +235,7 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
     }
     uint32_t want = 0;
     wf_put_shadow(shq, o32, ogrp, sh);
-    if (shadow_open<false>(S, &sh)) want |= kWfWantShadow;
+    want |= shadow_open<false>(S, &sh);   // the rays still open, one walk each
     if (trace) {
         wf_put_closest(cq, o32, ogrp, n32, ca);
         want |= kWfWantClosest;
@@ -260,6 +288,7 @@ PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfS
         sh.first[k] = S.n_tri;
     }
     sh.leak = shq->leak;
+    for (int k = 0; k < kLightSamples - 1; ++k) sh.occ[k] = sh.occ[k] | (shq->wocc[k] != 0);
     const D3 col = shadow_color<false>(S, W->obj, sh, nullptr);
     D3 acc = ld3(W->acc);
     double k = W->k;

@@ -94,7 +94,7 @@ int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
 // completion, as the GPU's shade / walk kernels do (split = 1, one slot per
 // pixel).  Must equal hc_render (force64 = 0, no counters) bit for bit.
 // steps_out (optional): shade steps that found work.
-// walk_stats (optional, int64[8]): shadow queries, node visits, leaves,
+// walk_stats (optional, int64[8]): shadow rays walked, node visits, leaves,
 // leaf units; the same for the closest walks.
 // depth_hist (optional, int64[2][32]): node visits of the shadow / closest
 // walks by QNode depth (root = 0)
@@ -167,29 +167,28 @@ int hc_render_wavefront2(const pt_scene_desc* d, const pt_render_params* p, doub
         ++busy;
         for (size_t i = 0; i < n; ++i) {
             const Spill sp{W[i].sp, 1};
-            if (want[i] & kWfWantShadow) {
-                ShadowSet sh;
+            for (int k = 0; k < kLightSamples; ++k) {   // one walk per open shadow ray, as k_wf_shadow
+                if (!((want[i] >> k) & 1u)) continue;
+                Shadow1 r;
                 F3 o32;
                 int ogrp;
-                wf_get_shadow(H.k, SQ[i], &o32, &ogrp, &sh);
-                ShadowTrav T;
+                wf_get_shadow1(SQ[i], k, &o32, &ogrp, &r);
+                ShadowTrav1 T;
                 int buf[kBvhStack];
                 const ShadowStack K{buf, 1};
-                strav_init<false>(T, H.k, o32, ogrp, &sh, H.k.qroot);
+                s1_init(T, H.k, o32, ogrp, r, H.k.qroot);
                 ++ws[0];
-                while (T.ref != kNoRef) {   // strav_step over the 4-wide nodes, counted
-                    while (T.ref >= 0) { hist(0, T.ref); strav_qnode<false>(T, K, H.k, &sh); ++ws[1]; }
+                while (T.ref != kNoRef) {   // the walk, counted
+                    while (T.ref >= 0) { hist(0, T.ref); s1_qnode(T, K, H.k, r); ++ws[1]; }
                     if (T.ref != kNoRef) {
                         ++ws[2];
                         ws[3] += (~T.ref) & 7;
-                        if (H.k.bunitc) strav_leaf<false, true>(T, K, H.k, &sh, sp, nullptr);   // as k_wf_shadow
-                        else strav_leaf<false>(T, K, H.k, &sh, sp, nullptr);
+                        if (H.k.bunitc) s1_units<true>(T, H.k, &r, sp, T.ref);
+                        else s1_units<false>(T, H.k, &r, sp, T.ref);
+                        T.ref = s1_pop(T, K, H.k, r);
                     }
                 }
-                int occ = 0;
-                for (int k = 0; k < kLightSamples; ++k) occ |= sh.occ[k] ? 1 << k : 0;
-                SQ[i].occ = occ;
-                SQ[i].leak = sh.leak;
+                wf_put_shadow1(&SQ[i], r);
             }
             if (want[i] & kWfWantClosest) {
                 ClosestAcc ca = wf_get_acc(CQ[i]);
