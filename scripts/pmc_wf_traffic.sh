@@ -5,9 +5,9 @@
 set -euo pipefail
 R=$PWD; OUT=$R/gpurun_out/pmc_wf_traffic; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/pf -o p -- python3 $R/scripts/k5_modes.py ${1:-512} ${2:-64} > $OUT/pf.log 2>&1
-timeout -k 10 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/pw -o p -- python3 $R/scripts/k5_modes.py ${1:-512} ${2:-64} > $OUT/pw.log 2>&1
-timeout -k 10 200 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d $OUT/ph -o p -- python3 $R/scripts/k5_modes.py ${1:-512} ${2:-64} > $OUT/ph.log 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/pf -o p -- python3 $R/scripts/prof_k5.py 1 ${1:-512} ${2:-64} > $OUT/pf.log 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/pw -o p -- python3 $R/scripts/prof_k5.py 1 ${1:-512} ${2:-64} > $OUT/pw.log 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d $OUT/ph -o p -- python3 $R/scripts/prof_k5.py 1 ${1:-512} ${2:-64} > $OUT/ph.log 2>&1
 for k in k_wf_shade k_wf_shadow k_wf_closest; do
   PMC_KERNEL=$k python3 $R/scripts/summarize_pmc.py $OUT/$k.json $OUT/pf $OUT/pw $OUT/ph > /dev/null
 done
