@@ -64,9 +64,11 @@ CONFIGS = {
                         "256 spp 4 bounces (BVH, wavefront kernels)"),
 }
 # k5 walk kernels' algorithmic bytes: a 4-wide node record
-# (QNode) per node visit, a leaf-unit record (UnitC) per leaf-unit test, the
-# query record read (WfShadowQ) and its 8-B result written per query
-QNODE_B, UNITC_B, SHADOWQ_B, SHADOW_RES_B = 64, 64, 96, 8
+# (QNode) per node visit, a leaf-unit record (UnitC) per leaf-unit test, and
+# per shadow ray (one query of the one-ray walks) its fields of the query
+# record read (origin, group, direction, range bracket, key2/leak: 44 B), the
+# list entry (4 B) and its result written (<= 8 B)
+QNODE_B, UNITC_B, SHADOWQ_B, SHADOW_RES_B = 64, 64, 48, 8
 
 
 def parse():
@@ -310,13 +312,13 @@ def k5_roofline(r, p, render_ms):
             "kernel": "k_wf_shadow<true,false> (persistent shadow walks)",
             "note": "latency-bound pointer chasing over an L2-resident BVH; HBM is the nearest "
                     "physical roof for its algorithmic bytes",
-            "work_per_launch": {"queries": wc["shadow_queries"] / nl,
+            "work_per_launch": {"shadow_rays": wc["shadow_queries"] / nl,
                                 "node_visits": wc["shadow_node_visits"] / nl,
                                 "leaf_unit_tests": wc["shadow_leaf_units"] / nl,
                                 "bytes": per_launch,
                                 "bytes_model": f"{QNODE_B} B per 4-wide node visit + {UNITC_B} B "
                                                f"per leaf unit + {SHADOWQ_B}+{SHADOW_RES_B} B "
-                                               f"per query"},
+                                               f"per shadow ray"},
             "kernel_ms_mean": round(launch_ms, 4), "launches_per_render": nl,
             "render_ms_mean": round(render_ms, 3),
             "kernel_ms_per_render": {"shade": round(kt["shade_ms"], 2),

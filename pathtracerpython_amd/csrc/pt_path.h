@@ -1203,6 +1203,28 @@ struct Shadow1 {
 PT_HD bool shadow1_open(const SceneK& S, const Shadow1& r) {
     return r.k == kLightSamples - 1 ? r.key2 > S.bvh_min_obj : !r.occ;
 }
+// the f64 decisions of a unit's ambiguous tests for the ray (a0, a1)
+// (inline: an out-of-line call's frame made the walk 2x slower)
+PT_HD void shadow1_fallback(const SceneK& S, const UnitF& U, bool a0, bool a1, Shadow1* r,
+                      const Spill& sp) {
+    const bool last = r->k == kLightSamples - 1;
+    const D3 P = sp.get3(kSpP);
+    const D3 L = sp.get3(kSpL + 3 * r->k);
+    for (int i = 0; i < 2; ++i) {
+        if (!(i == 0 ? a0 : a1)) continue;
+        if (last ? (U.obj >= r->key2) : r->occ) continue;   // decided meanwhile
+        D3 Q;
+        double sqd;
+        if (eval64(S.trid[U.t[i]], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
+            sqd < squared_dist(P, L)) {
+            r->occ = true;
+            if (last) {
+                r->key2 = U.obj;
+                r->leak = U.obj;
+            }
+        }
+    }
+}
 // one BVH unit against the ray (fused_unit's shadow part for one ray, its
 // f64 fallback included: same verdicts, same decisions)
 PT_HD void shadow1_unit(const SceneK& S, const UnitF& U, F3 o32, int ogrp, Shadow1* r,
@@ -1228,24 +1250,7 @@ PT_HD void shadow1_unit(const SceneK& S, const UnitF& U, F3 o32, int ogrp, Shado
             r->leak = U.obj;
         }
     }
-    if (need && (a0 | a1)) {
-        const D3 P = sp.get3(kSpP);
-        const D3 L = sp.get3(kSpL + 3 * r->k);
-        for (int i = 0; i < 2; ++i) {
-            if (!(i == 0 ? a0 : a1)) continue;
-            if (last ? (U.obj >= r->key2) : r->occ) continue;   // decided meanwhile
-            D3 Q;
-            double sqd;
-            if (eval64(S.trid[U.t[i]], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
-                sqd < squared_dist(P, L)) {
-                r->occ = true;
-                if (last) {
-                    r->key2 = U.obj;
-                    r->leak = U.obj;
-                }
-            }
-        }
-    }
+    if (need && (a0 | a1)) shadow1_fallback(S, U, a0, a1, r, sp);
 }
 struct ShadowTrav1 {
     F3 o32, inv;
