@@ -52,6 +52,9 @@ SEED = 9
 FLOP_PER_TEST = 47          # Moller-Trumbore with line semantics
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector (VALU) peak
 HBM_PEAK_GBS = 8000.0
+# MI355X_MICROARCH.md "Indexed rows": rows served from the XCDs' L2, gathered
+# by every CU, 16.8-18.8 TB/s chip-wide (a measured lower bound of the L2 roof)
+L2_GATHER_PEAK_GBS = 18800.0
 METRIC = "Mega path-samples/sec on Cornell box; per-pixel L-inf vs CPU ref"
 
 CONFIGS = {
@@ -290,9 +293,12 @@ def k_render_roofline(r, p, k_ms, W, rows, SPP, config):
 
 
 def k5_roofline(r, p, render_ms):
-    """The wavefront render's dominant kernel (the shadow walks, k_wf_shadow)
-    against HBM: algorithmic bytes of its launches (counting launch) over
-    their HIP-event time (a profiling launch of the production kernels)."""
+    """The wavefront render's dominant kernel (the shadow walks, k_wf_shadow):
+    algorithmic bytes of its launches (counting launch) over their HIP-event
+    time (a profiling launch of the production kernels), against the L2 roof —
+    the BVH (7.5 MB) is served from the XCDs' L2 (91% hit) and the rate of its
+    record reads exceeds HBM's peak; the PMC traffic beyond L2 is reported
+    beside it as hbm_frac."""
     from pathtracerpython_amd._abi import PT_FLAG_KERNEL_TIMES, PT_FLAG_WALK_COUNT, make_params
 
     def with_flags(f):
@@ -307,11 +313,14 @@ def k5_roofline(r, p, render_ms):
     launch_ms = kt["shadow_ms"] / nl
     achieved = per_launch / (launch_ms * 1e-3) / 1e9
     traffic, tsrc = load_traffic("k5")
-    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "k_wf_shadow<true,false> (persistent shadow walks)",
-            "note": "latency-bound pointer chasing over an L2-resident BVH; HBM is the nearest "
-                    "physical roof for its algorithmic bytes",
+    return {"bound": "l2", "achieved": round(achieved, 2), "peak": L2_GATHER_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / L2_GATHER_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "k_wf_shadow<true,false> (persistent one-ray shadow walks)",
+            "note": "latency-bound pointer chasing over an L2-resident BVH: the peak is the "
+                    "L2-served gather rate of MI355X_MICROARCH.md (16.8-18.8 TB/s); the record "
+                    "reads run above HBM's 8 TB/s, the PMC bytes beyond L2 are traffic / hbm_frac",
+            "hbm_frac": (round(traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                         if traffic else None),
             "work_per_launch": {"shadow_rays": wc["shadow_queries"] / nl,
                                 "node_visits": wc["shadow_node_visits"] / nl,
                                 "leaf_unit_tests": wc["shadow_leaf_units"] / nl,

@@ -13,12 +13,16 @@ for d in dirs:
             meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                                       "Scratch_Size", "VGPR_Count", "SGPR_Count")}
 res = {"kernel": meta, "per_dispatch_median": {k: statistics.median(v) for k, v in agg.items()},
+       "per_dispatch_mean": {k: statistics.mean(v) for k, v in agg.items()},
        "sum_over_dispatches": {k: sum(v) for k, v in agg.items()},
        "dispatches": {k: len(v) for k, v in agg.items()}}
 if "FETCH_SIZE" in agg or "WRITE_SIZE" in agg:
     fk = res["per_dispatch_median"].get("FETCH_SIZE", 0.0)
     wk = res["per_dispatch_median"].get("WRITE_SIZE", 0.0)
     res["hbm_bytes_per_launch"] = int(round(fk * 1024 * 2 + wk * 1024))
+    fm = res["per_dispatch_mean"].get("FETCH_SIZE", 0.0)
+    wm = res["per_dispatch_mean"].get("WRITE_SIZE", 0.0)
+    res["hbm_bytes_per_launch_mean"] = int(round(fm * 1024 * 2 + wm * 1024))
     res["hbm_note"] = ("FETCH_SIZE/WRITE_SIZE are KiB per dispatch from separate --pmc passes; "
                        "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half of wide reads); "
                        "WRITE_SIZE exact (framebuffer 512x512x3 f32 = 3,145,728 B)")
