@@ -273,9 +273,9 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
             want = wf_start(S, j.J, j.d0, &W[tid], &CQ[tid]);
         } else {
             W[tid].acc[0] = W[tid].acc[1] = W[tid].acc[2] = 0.0;
-            W[tid].state = kWfDone;
+            W[tid].set(kWfDone, false, 0);
         }
-    } else if (j.valid && W[tid].state != kWfDone) {
+    } else if (j.valid && W[tid].state() != kWfDone) {
         want = wf_shade(S, j.J, j.d0, &W[tid], &SQ[tid], &CQ[tid]);
     }
     wf_append3(want, &counters[0], lists, (int32_t)tid);   // one shadow walk per open ray
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
 #ifndef PT_WALK_STACK_LDS
 #define PT_WALK_STACK_LDS 16
 #endif
-constexpr int kWalkStack = 32;                   // entries of a walk kernel's stack
+constexpr int kWalkStack = 48;                   // entries of a walk kernel's stack (= kBvhStack)
 constexpr int kWalkStackLds = PT_WALK_STACK_LDS;  // of them in shared memory
 constexpr int kWalkStackGlobal = kWalkStack - kWalkStackLds;
 // COUNT (PT_FLAG_WALK_COUNT launches only): per-query work of the walk —

@@ -57,7 +57,10 @@ struct Spill {
     PT_HD void put3(int i, D3 v) const { put(i, v.x); put(i + 1, v.y); put(i + 2, v.z); }
 };
 constexpr int kSpillSlots = 20;
-constexpr int kSpL = 0, kSpNd = 9, kSpP = 12, kSpD0 = 15, kSpP0 = 17;
+// P and Nd first: the wavefront path record (pt_wavefront.h WfPath) keeps them
+// in the same 128-B line as the per-step fields; the light points and the
+// primary hit follow in the other line
+constexpr int kSpP = 0, kSpNd = 3, kSpL = 6, kSpD0 = 15, kSpP0 = 17;
 
 // ----------------------------------------------------------- closest hit --
 // intersect_objects (main.py:83-122): the triangle whose intersection has the

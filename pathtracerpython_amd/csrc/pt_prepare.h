@@ -35,7 +35,13 @@ struct HostScene {
 };
 
 constexpr int kBvhMinTris = 64;   // objects this large are traversed through the BVH
-constexpr int kBvhLeaf = 2;       // units per leaf (at most 7: 3 bits of BNode::leaf)
+// Units per leaf: 1 since the one-ray shadow walks (K5 512^2 x 64: 1 / 2 / 3 /
+// 4 -> 93.2 / 94.6 / 100.9 / 107.8 ms; a unit test costs about a third of a
+// node visit, but a leaf box prunes its unit before its record is loaded)
+#ifndef PT_BVH_LEAF
+#define PT_BVH_LEAF 1
+#endif
+constexpr int kBvhLeaf = PT_BVH_LEAF;   // units per leaf (at most 7: 3 bits of BNode::leaf)
 constexpr int kBvhBins = 16;
 constexpr int kBvhStackHost = 48;   // = kBvhStack (pt_path.h)
 

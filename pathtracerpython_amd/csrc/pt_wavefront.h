@@ -24,21 +24,34 @@
 // Path state lives in HBM between the kernels: WfPath (256 B per slot, the
 // f64 spill home included) and the query records.
 #pragma once
+#include <stddef.h>
+
 #include "pt_path.h"
 
 namespace pt {
 
 enum : int32_t { kWfDone = 0, kWfPrimary = 1, kWfBounce = 2 };
 
-struct alignas(16) WfPath {
-    double sp[kSpillSlots];   // the spill home of pt_path.h (Spill{sp, 1})
+// Two 128-B lines per slot: the first holds everything a shade step reads
+// and writes (the per-step fields and the spill slots P, Nd), the second the
+// light points (written per bounce, read only by f64 fallbacks) and the
+// primary hit (read when a sample restarts).
+struct alignas(128) WfPath {
     double acc[3];            // sum of this slot's sample colours
     double k, kk;             // throughput before / after the pending bounce
     double ln[kLightSamples]; // l_k . n of the pending bounce's light samples
-    int32_t state, si, b, tri;
-    int32_t tri0, obj, trace, pad;
+    int32_t tri, tri0, si;    // the pending bounce's triangle, the primary hit's, the sample
+    uint32_t sb;              // state | trace << 2 | b << 3 (the bounce index)
+    double sp[kSpillSlots];   // the spill home of pt_path.h (Spill{sp, 1}): P, Nd | L, D0, P0
+    double pad[2];
+    PT_HD int state() const { return (int)(sb & 3u); }
+    PT_HD bool trace() const { return ((sb >> 2) & 1u) != 0; }
+    PT_HD int b() const { return (int)(sb >> 3); }
+    PT_HD void set(int state, bool trace, int b) { sb = (uint32_t)state | (trace ? 4u : 0u) | ((uint32_t)b << 3); }
 };
 static_assert(sizeof(WfPath) == 256, "WfPath is 256 B");
+static_assert(offsetof(WfPath, sp) + (kSpNd + 3) * sizeof(double) <= 128,
+              "P and Nd in the first line");
 
 // shadow walks: in = the state after the uniform units, out = the final
 // state.  The one-ray walks of a query write disjoint fields: ray 0 / 1 its
@@ -143,7 +156,7 @@ enum : uint32_t { kWfWantShadow = 7u, kWfWantClosest = 8u };
 // does for it in k_render; the BVH part is a closest query.
 PT_HD uint32_t wf_start(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfClosestQ* cq) {
     W->acc[0] = W->acc[1] = W->acc[2] = 0.0;
-    W->state = kWfDone;
+    W->set(kWfDone, false, 0);
     if (J.n_samples <= 0 || J.bounces <= 0) return 0;   // main.py:192 never runs
     const Spill sp{W->sp, 1};
     const D3 eye = ld3(S.eye);
@@ -159,7 +172,7 @@ PT_HD uint32_t wf_start(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfC
                             nullptr);
     }
     wf_put_closest(cq, o32, -1, d32, acc);
-    W->state = kWfPrimary;
+    W->set(kWfPrimary, false, 0);
     return kWfWantClosest;
 }
 
@@ -169,7 +182,7 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
                                WfClosestQ* cq) {
     const Spill sp{W->sp, 1};
     const D3 P = sp.get3(kSpP);
-    const int tri = W->tri, b = W->b;
+    const int tri = W->tri, b = W->b();
     const uint32_t sample = (uint32_t)(J.sample0 + W->si * J.sample_stride);
     const int obj = S.tri_obj[tri];
     const TriS R = S.tris[tri];
@@ -242,10 +255,8 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
     }
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) W->ln[k] = sh.ln[k];
-    W->obj = obj;
     W->kk = kk;
-    W->trace = trace ? 1 : 0;
-    W->state = kWfBounce;
+    W->set(kWfBounce, trace, b);
     return want;
 }
 
@@ -254,7 +265,7 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
 PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfShadowQ* shq,
                         WfClosestQ* cq) {
     const Spill sp{W->sp, 1};
-    if (W->state == kWfPrimary) {   // k_render: closest(eye, d0) then render_lane's prologue
+    if (W->state() == kWfPrimary) {   // k_render: closest(eye, d0) then render_lane's prologue
         D3 P0 = d3(0, 0, 0);
         const int tri0 = closest_finish<false, false, true>(S, wf_get_acc(*cq), sp.get3(kSpP),
                                                             unit(sp.get3(kSpNd)), &P0, nullptr);
@@ -263,11 +274,11 @@ PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfS
             D3 acc = d3(0, 0, 0);
             for (int i = 0; i < J.n_samples; ++i) acc = acc + v;
             W->acc[0] = acc.x; W->acc[1] = acc.y; W->acc[2] = acc.z;
-            W->state = kWfDone;
+            W->set(kWfDone, false, 0);
             return 0;
         }
         W->si = 0;
-        W->b = 0;
+        W->set(kWfPrimary, false, 0);   // (b = 0; begin_bounce sets the state)
         W->tri = tri0;
         W->tri0 = tri0;
         W->k = 1.0;
@@ -278,7 +289,7 @@ PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfS
         sp.put3(kSpNd, d0);   // incoming direction of bounce 0 (main.py:191)
         return wf_begin_bounce(S, J, W, shq, cq);
     }
-    if (W->state != kWfBounce) return 0;
+    if (W->state() != kWfBounce) return 0;
     // the colour of the pending bounce (main.py:208-231)
     ShadowSet sh;
 #pragma unroll
@@ -289,13 +300,13 @@ PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfS
     }
     sh.leak = shq->leak;
     for (int k = 0; k < kLightSamples - 1; ++k) sh.occ[k] = sh.occ[k] | (shq->wocc[k] != 0);
-    const D3 col = shadow_color<false>(S, W->obj, sh, nullptr);
+    const D3 col = shadow_color<false>(S, S.tri_obj[W->tri], sh, nullptr);   // the pending bounce's object
     D3 acc = ld3(W->acc);
     double k = W->k;
     acc = acc + col * k;   // main.py:230-231 (k before this bounce's update)
     k = W->kk;
-    bool done = W->trace == 0;
-    int tri = W->tri, b = W->b, si = W->si;
+    bool done = !W->trace();
+    int tri = W->tri, b = W->b(), si = W->si;
     if (!done) {
         D3 Pn;
         const int tn = closest_finish<false, false, true>(S, wf_get_acc(*cq), sp.get3(kSpP),
@@ -323,12 +334,12 @@ PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfS
     W->acc[0] = acc.x; W->acc[1] = acc.y; W->acc[2] = acc.z;
     W->k = k;
     W->tri = tri;
-    W->b = b;
     W->si = si;
     if (si >= J.n_samples) {
-        W->state = kWfDone;
+        W->set(kWfDone, false, 0);
         return 0;
     }
+    W->set(kWfBounce, false, b);   // (begin_bounce sets trace)
     return wf_begin_bounce(S, J, W, shq, cq);
 }
 
