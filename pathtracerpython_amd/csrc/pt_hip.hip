@@ -743,10 +743,11 @@ static int validate(const pt_render_params* p) {
 //
 // Single kernel: >= 8 samples per lane, at most 2^30 lanes over the full
 // image (K2 512^2 x 64 spp: 8 lanes per pixel; K3 and K4: 64).
-// Wavefront (BVH scenes): path slots hold ~400 B of state each, so at most
-// 16M slots over the full image (K5 512^2 x 64 spp: 2M slots 161.6 ms, 4M
-// 147.1, 8M 140.5, 16M 139.3; 1024^2 x 256 spp: 2M 2586 ms, 16M 2096); an
-// N-way band gets 1/N of them.  The single kernel uses the same split on BVH
+// Wavefront (BVH scenes): path slots hold ~420 B of state each, so at most
+// 64M slots (28 GB) over the full image (K5 512^2 x 64 spp: 2M slots 161.6
+// ms, 4M 147.1, 8M 140.5, 16M 139.3 (round 1); 1024^2 x 256 spp with the
+// one-ray walks: 16M 1419 ms, 32M 1392, 64M 1378 — fewer shade / walk steps,
+// each with its drain); an N-way band gets 1/N of them.  The single kernel uses the same split on BVH
 // scenes, so its framebuffer stays bitwise equal to the wavefront one.
 //
 // PT_SPLIT_FIXED (compile-time, tuning builds only) pins the split.
@@ -760,7 +761,7 @@ static uint32_t choose_split(uint64_t image_pixels, int32_t spp, bool bvh) {
     return f;
 #else
     uint32_t s = 1;
-    const uint64_t target = (uint64_t)1 << (bvh ? 24 : 30);
+    const uint64_t target = (uint64_t)1 << (bvh ? 26 : 30);
     while (s < cap && image_pixels * s * 2 <= target && (bvh || spp / (int32_t)(s * 2) >= 8)) s *= 2;
     return s;
 #endif
