@@ -776,11 +776,14 @@ static uint32_t choose_split(uint64_t image_pixels, int32_t spp, bool bvh) {
 // Round 2 re-sweep (512^2 x 64 spp render, both walks): 16 / 24 / 32 / 40 /
 // 48 -> 114.3 / 110.5 / 108.0 / 107.8 / 109.5 ms; the one-ray shadow walk's
 // threshold 16 / 24 / 32 / 40 / 48 -> 100.7 / 98.8 / 97.4 / 96.9 / 96.9 ms.
+// At the K5 bench size with 64M slots (1024^2 x 256 spp, ms): shadow / closest
+// 40/32 1372-1382, 32/32 1407, 48/32 1366, 40/40 1370, 48/40 1349, 48/48
+// 1351, 56/48 1359, 64/56 1885 (64: the node phase never ends early).
 #ifndef PT_WF_THR_SHADOW
-#define PT_WF_THR_SHADOW 40
+#define PT_WF_THR_SHADOW 48
 #endif
 #ifndef PT_WF_THR_CLOSEST
-#define PT_WF_THR_CLOSEST 32
+#define PT_WF_THR_CLOSEST 40
 #endif
 #ifndef PT_WF_SHADOW_BLOCKS_PER_CU
 #define PT_WF_SHADOW_BLOCKS_PER_CU 5
