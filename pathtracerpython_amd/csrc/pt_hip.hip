@@ -260,23 +260,35 @@ __device__ __forceinline__ int32_t wf_fetch(bool need, int32_t* head, int32_t& c
     return pos;
 }
 
+// The primary rays: one work-item per pixel (a pixel's `split` slots share
+// it, main.py:191): the uniform part of the eye ray into CQP[pixel], whose
+// BVH part is a closest query (list entry = pixel; spill home = the pixel's
+// first slot).  Every slot of the pixel finishes it in its first shade step.
+__global__ __launch_bounds__(256) void k_wf_primary(SceneK S, RenderK R, WfPath* __restrict__ W,
+                                                    WfClosestQ* __restrict__ CQP,
+                                                    int32_t* __restrict__ list, int32_t* counters) {
+    const uint32_t pix = blockIdx.x * 256u + threadIdx.x;
+    uint32_t want = 0;
+    if (pix < R.npix) {
+        const uint32_t slot = pix << R.split_log2;
+        const SlotJob j = slot_job(S, R, slot);
+        if (j.valid) want = wf_start(S, j.J, j.d0, &W[slot], &CQP[pix]);
+    }
+    wf_append((want & kWfWantClosest) != 0, counters, list, (int32_t)pix);
+}
 __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t step,
                                                   WfPath* __restrict__ W, WfShadowQ* __restrict__ SQ,
-                                                  WfClosestQ* __restrict__ CQ,
+                                                  WfClosestQ* __restrict__ CQ, const WfClosestQ* __restrict__ CQP,
                                                   int32_t* __restrict__ lists, int32_t* counters,
                                                   uint32_t slots) {
     const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
     const SlotJob j = slot_job(S, R, tid);
     uint32_t want = 0;
-    if (step == 0) {
-        if (j.valid) {
-            want = wf_start(S, j.J, j.d0, &W[tid], &CQ[tid]);
-        } else {
-            W[tid].acc[0] = W[tid].acc[1] = W[tid].acc[2] = 0.0;
-            W[tid].set(kWfDone, false, 0);
-        }
+    if (step == 0) {   // the primary queries are k_wf_primary's (one per pixel)
+        W[tid].acc[0] = W[tid].acc[1] = W[tid].acc[2] = 0.0;
+        W[tid].set(j.valid && j.J.n_samples > 0 && j.J.bounces > 0 ? kWfPrimary : kWfDone, false, 0);
     } else if (j.valid && W[tid].state() != kWfDone) {
-        want = wf_shade(S, j.J, j.d0, &W[tid], &SQ[tid], &CQ[tid]);
+        want = wf_shade(S, j.J, j.d0, &W[tid], &SQ[tid], &CQ[tid], &CQP[tid >> R.split_log2]);
     }
     wf_append3(want, &counters[0], lists, (int32_t)tid);   // one shadow walk per open ray
     wf_append((want & kWfWantClosest) != 0, &counters[2], lists + 3 * (size_t)slots, (int32_t)tid);
@@ -414,7 +426,10 @@ __global__ __launch_bounds__(256, PT_CLOSEST_WAVES) void k_wf_closest(SceneK S, 
                                                     const int32_t* __restrict__ list, int32_t* counters,
                                                     int32_t thr, unsigned long long* wc,
                                                     int* __restrict__ ovf_ref,
-                                                    uint16_t* __restrict__ ovf_dist) {
+                                                    uint16_t* __restrict__ ovf_dist,
+                                                    uint32_t wshift) {
+    // wshift: list entries index CQ; the spill home of entry e is
+    // W[e << wshift] (the primary queries: one per pixel, its first slot's home)
     uint32_t c_q = 0, c_nodes = 0, c_units = 0;
     const int32_t count = counters[0];   // [count, head]
     int32_t cb = 0, ce = 0;   // this wave's claimed list positions (wf_fetch)
@@ -464,7 +479,7 @@ __global__ __launch_bounds__(256, PT_CLOSEST_WAVES) void k_wf_closest(SceneK S, 
             }
         }
         if (slot >= 0) {
-            const Spill sp{W[slot].sp, 1};
+            const Spill sp{W[(size_t)slot << wshift].sp, 1};
             if (COUNT)
                 c_units += (pl != kNoRef ? leaf_units(pl) : 0u) + (pl2 != kNoRef ? leaf_units(pl2) : 0u) +
                            (T.ref <= -2 ? leaf_units(T.ref) : 0u);
@@ -816,7 +831,9 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
                  sz_ocd = ovf_n * cl_blocks * 256 * 2;
     const size_t off_s = sz_w, off_c = off_s + sz_s, off_l = off_c + sz_c, off_n = off_l + sz_l;
     const size_t off_os = off_n + 256, off_ocr = off_os + sz_os, off_ocd = off_ocr + sz_ocr;
-    const size_t need = off_ocd + sz_ocd + 256;
+    const size_t sz_p = (size_t)R.npix * sizeof(WfClosestQ);   // the primary queries, per pixel
+    const size_t off_p = (off_ocd + sz_ocd + 255) / 256 * 256;
+    const size_t need = off_p + sz_p + 256;
     if (need > s->wf_bytes) {
         if (s->wf) (void)hipFree(s->wf);
         s->wf = nullptr;
@@ -838,6 +855,7 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     int* ovf_s = (int*)(b + off_os);
     int* ovf_cr = (int*)(b + off_ocr);
     uint16_t* ovf_cd = (uint16_t*)(b + off_ocd);
+    WfClosestQ* CQP = (WfClosestQ*)(b + off_p);
     const int32_t per_slot = (R.spp + (int32_t)R.split - 1) / (int32_t)R.split;
     const int32_t steps = per_slot * R.bounces + 2;
     const bool wcount = (flags & PT_FLAG_WALK_COUNT) != 0 && stats;
@@ -856,14 +874,17 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     auto mark = [&](int32_t step, int k, int end, hipStream_t on) -> hipError_t {
         return times ? hipEventRecord(s->prof_ev[(size_t)step * 6 + k * 2 + end], on) : hipSuccess;
     };
-    auto closest_walk = [&](hipStream_t on) {
+    // step 0 walks the primary queries (CQP, one per pixel), later steps the slots' (CQ)
+    auto closest_walk = [&](hipStream_t on, int32_t step) {
         const int32_t* l = lists + 3 * slots;
+        WfClosestQ* q = step == 0 ? CQP : CQ;
+        const uint32_t ws = step == 0 ? R.split_log2 : 0u;
         if (s->dev.bunitc) {
-            if (wcount) hipLaunchKernelGGL((k_wf_closest<true, true>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd);
-            else hipLaunchKernelGGL((k_wf_closest<true, false>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd);
+            if (wcount) hipLaunchKernelGGL((k_wf_closest<true, true>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, q, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd, ws);
+            else hipLaunchKernelGGL((k_wf_closest<true, false>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, q, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd, ws);
         } else {
-            if (wcount) hipLaunchKernelGGL((k_wf_closest<false, true>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd);
-            else hipLaunchKernelGGL((k_wf_closest<false, false>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, CQ, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd);
+            if (wcount) hipLaunchKernelGGL((k_wf_closest<false, true>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, q, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd, ws);
+            else hipLaunchKernelGGL((k_wf_closest<false, false>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, q, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd, ws);
         }
     };
     auto shadow_walk = [&](hipStream_t on) {
@@ -880,8 +901,11 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     for (int32_t step = 0; step < steps; ++step) {
         HIPCHK(hipMemsetAsync(counters, 0, 4 * sizeof(int32_t), st));
         HIPCHK(mark(step, 0, 0, st));
-        hipLaunchKernelGGL(k_wf_shade, grid, dim3(256), 0, st, s->dev, R, step, W, SQ, CQ, lists,
-                           counters, (uint32_t)slots);
+        hipLaunchKernelGGL(k_wf_shade, grid, dim3(256), 0, st, s->dev, R, step, W, SQ, CQ,
+                           (const WfClosestQ*)CQP, lists, counters, (uint32_t)slots);
+        if (step == 0)
+            hipLaunchKernelGGL(k_wf_primary, dim3((R.npix + 255) / 256), dim3(256), 0, st, s->dev, R, W,
+                               CQP, lists + 3 * slots, counters + 2);
         HIPCHK(mark(step, 0, 1, st));
         if (step + 1 < steps) {
             // the two walks only read the shade step's output and write
@@ -892,7 +916,7 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
                 HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
             }
             HIPCHK(mark(step, 2, 0, cs));
-            closest_walk(cs);
+            closest_walk(cs, step);
             HIPCHK(mark(step, 2, 1, cs));
             if (PT_WF_CONCURRENT) HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
             HIPCHK(mark(step, 1, 0, st));

@@ -262,13 +262,15 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
 
 // Shade step >= 1: finish the pending work of the slot with the walks'
 // results, then start its next bounce.  Returns the queries wanted.
+// pq: the slot's primary query (the GPU shares one per pixel, k_wf_primary;
+// the host emulation has one per slot, cq)
 PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfShadowQ* shq,
-                        WfClosestQ* cq) {
+                        WfClosestQ* cq, const WfClosestQ* pq) {
     const Spill sp{W->sp, 1};
     if (W->state() == kWfPrimary) {   // k_render: closest(eye, d0) then render_lane's prologue
         D3 P0 = d3(0, 0, 0);
-        const int tri0 = closest_finish<false, false, true>(S, wf_get_acc(*cq), sp.get3(kSpP),
-                                                            unit(sp.get3(kSpNd)), &P0, nullptr);
+        const int tri0 = closest_finish<false, false, true>(S, wf_get_acc(*pq), ld3(S.eye), unit(d0),
+                                                            &P0, nullptr);
         if (tri0 < 0 || tri0 >= S.n_obj_tri) {   // primary ray escapes or hits the light
             const D3 v = tri0 < 0 ? d3(0, 0, 0) : ld3(S.light_rgb);
             D3 acc = d3(0, 0, 0);

@@ -159,7 +159,7 @@ int hc_render_wavefront2(const pt_scene_desc* d, const pt_render_params* p, doub
             want[i] = 0;
             if (step == 0) want[i] = wf_start(H.k, J[i], D0[i], &W[i], &CQ[i]);
             else if (W[i].state() != kWfDone) {
-                want[i] = wf_shade(H.k, J[i], D0[i], &W[i], &SQ[i], &CQ[i]);
+                want[i] = wf_shade(H.k, J[i], D0[i], &W[i], &SQ[i], &CQ[i], &CQ[i]);
                 any = true;
             }
         }
