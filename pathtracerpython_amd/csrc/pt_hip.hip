@@ -282,12 +282,14 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
                                                   int32_t* __restrict__ lists, int32_t* counters,
                                                   uint32_t slots) {
     const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
-    const SlotJob j = slot_job(S, R, tid);
     uint32_t want = 0;
     if (step == 0) {   // the primary queries are k_wf_primary's (one per pixel)
+        const SlotJob j = slot_job(S, R, tid);
         W[tid].acc[0] = W[tid].acc[1] = W[tid].acc[2] = 0.0;
         W[tid].set(j.valid && j.J.n_samples > 0 && j.J.bounces > 0 ? kWfPrimary : kWfDone, false, 0);
-    } else if (j.valid && W[tid].state() != kWfDone) {
+    } else if ((tid >> R.split_log2) < R.npix && W[tid].state() != kWfDone) {
+        // (a finished slot costs one load: its job is only built when it runs)
+        const SlotJob j = slot_job(S, R, tid);
         want = wf_shade(S, j.J, j.d0, &W[tid], &SQ[tid], &CQ[tid], &CQP[tid >> R.split_log2]);
     }
     wf_append3(want, &counters[0], lists, (int32_t)tid);   // one shadow walk per open ray
