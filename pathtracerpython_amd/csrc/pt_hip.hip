@@ -230,6 +230,60 @@ __device__ __forceinline__ void wf_append3(uint32_t want, int32_t* counter, int3
     for (int k = 0; k < kLightSamples; ++k)
         if ((want >> k) & 1u) list[pos++] = wf_shadow_entry(slot, k);
 }
+// Both lists' appends of a 256-work-item block with one atomic per list and
+// block: every block's appends land on the same two counters, whose atomics
+// serialise (~10 ns each: three per wave on one counter made the shade step
+// 6 -> 11.6 ms at 262k waves).  Entries as wf_append3 / wf_append, the
+// block's waves in order.
+#ifndef PT_WF_BLOCK_APPEND
+#define PT_WF_BLOCK_APPEND 1
+#endif
+// work-items per shade block (one append atomic per list and block): 256 /
+// 512 / 1024 -> K5 1248 / 1255 / 1284 ms (512: two waves/SIMD at 135 VGPRs;
+// 1024: 127 VGPRs with a spill)
+#ifndef PT_SHADE_BLOCK
+#define PT_SHADE_BLOCK 256
+#endif
+constexpr int kShadeBlock = PT_SHADE_BLOCK;
+static_assert(kShadeBlock % 64 == 0 && kShadeBlock <= 1024, "whole waves");
+__device__ __forceinline__ void wf_append_block(uint32_t want, int32_t* counters, int32_t* shadow_list,
+                                                int32_t* closest_list, int32_t slot) {
+    constexpr int kWaves = kShadeBlock / 64;
+    __shared__ int32_t cnt[2][kWaves], base[2];
+    uint64_t m[kLightSamples];
+    int32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        m[k] = __ballot(((want >> k) & 1u) != 0);
+        n += (int32_t)__popcll(m[k]);
+    }
+    const uint64_t mc = __ballot((want & kWfWantClosest) != 0);
+    const int wv = (int)(threadIdx.x >> 6);
+    if ((threadIdx.x & 63u) == 0) {
+        cnt[0][wv] = n;
+        cnt[1][wv] = (int32_t)__popcll(mc);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 || threadIdx.x == 64) {   // the two atomics from two waves
+        const int l = threadIdx.x == 0 ? 0 : 1;
+        int32_t tot = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) tot += cnt[l][w];
+        base[l] = tot ? atomicAdd(&counters[2 * l], tot) : 0;
+    }
+    __syncthreads();
+    int32_t bs = base[0], bc = base[1];
+    for (int w = 0; w < wv; ++w) {
+        bs += cnt[0][w];
+        bc += cnt[1][w];
+    }
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) bs += (int32_t)lanes_below(m[k]);
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k)
+        if ((want >> k) & 1u) shadow_list[bs++] = wf_shadow_entry(slot, k);
+    if (want & kWfWantClosest) closest_list[bc + (int32_t)lanes_below(mc)] = slot;
+}
 // Next list positions for the lanes that need one.  A wave claims a chunk of
 // kWfChunk consecutive positions with one atomic on the list head and hands
 // them out to its lanes as they need work; it claims the next chunk only when
@@ -276,14 +330,15 @@ __global__ __launch_bounds__(256) void k_wf_primary(SceneK S, RenderK R, WfPath*
     }
     wf_append((want & kWfWantClosest) != 0, counters, list, (int32_t)pix);
 }
-__global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t step,
+__global__ __launch_bounds__(kShadeBlock) void k_wf_shade(SceneK S, RenderK R, int32_t step,
                                                   WfPath* __restrict__ W, WfShadowQ* __restrict__ SQ,
                                                   WfClosestQ* __restrict__ CQ, const WfClosestQ* __restrict__ CQP,
                                                   int32_t* __restrict__ lists, int32_t* counters,
                                                   uint32_t slots) {
-    const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t tid = blockIdx.x * (uint32_t)kShadeBlock + threadIdx.x;
     uint32_t want = 0;
-    if (step == 0) {   // the primary queries are k_wf_primary's (one per pixel)
+    if (tid >= slots) {   // (the last block of a kShadeBlock grid over 256-slot blocks)
+    } else if (step == 0) {   // the primary queries are k_wf_primary's (one per pixel)
         const SlotJob j = slot_job(S, R, tid);
         W[tid].acc[0] = W[tid].acc[1] = W[tid].acc[2] = 0.0;
         W[tid].set(j.valid && j.J.n_samples > 0 && j.J.bounces > 0 ? kWfPrimary : kWfDone, false, 0);
@@ -292,8 +347,12 @@ __global__ __launch_bounds__(256) void k_wf_shade(SceneK S, RenderK R, int32_t s
         const SlotJob j = slot_job(S, R, tid);
         want = wf_shade(S, j.J, j.d0, &W[tid], &SQ[tid], &CQ[tid], &CQP[tid >> R.split_log2]);
     }
+#if PT_WF_BLOCK_APPEND
+    wf_append_block(want, counters, lists, lists + 3 * (size_t)slots, (int32_t)tid);
+#else
     wf_append3(want, &counters[0], lists, (int32_t)tid);   // one shadow walk per open ray
     wf_append((want & kWfWantClosest) != 0, &counters[2], lists + 3 * (size_t)slots, (int32_t)tid);
+#endif
 }
 
 // Persistent walk kernels over the 4-wide quantised BVH (QNode): a
@@ -903,7 +962,8 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     for (int32_t step = 0; step < steps; ++step) {
         HIPCHK(hipMemsetAsync(counters, 0, 4 * sizeof(int32_t), st));
         HIPCHK(mark(step, 0, 0, st));
-        hipLaunchKernelGGL(k_wf_shade, grid, dim3(256), 0, st, s->dev, R, step, W, SQ, CQ,
+        hipLaunchKernelGGL(k_wf_shade, dim3((unsigned)((slots + kShadeBlock - 1) / kShadeBlock)),
+                           dim3(kShadeBlock), 0, st, s->dev, R, step, W, SQ, CQ,
                            (const WfClosestQ*)CQP, lists, counters, (uint32_t)slots);
         if (step == 0)
             hipLaunchKernelGGL(k_wf_primary, dim3((R.npix + 255) / 256), dim3(256), 0, st, s->dev, R, W,
