@@ -9,7 +9,7 @@ CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 OUT = os.path.join(HERE, "_lib", "libpt_hip.so")
 SOURCES = ["pt_hip.hip"]
-DEPS = SOURCES + ["pt_core.h", "pt_math.h", "pt_path.h", "pt_prepare.h", "pt_image.h", "pt_ingest.h"]
+DEPS = SOURCES + ["pt_core.h", "pt_math.h", "pt_path.h", "pt_prepare.h", "pt_image.h", "pt_ingest.h", "pt_wavefront.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # -ffp-contract=off: every f64 operation rounds separately, as the reference's
