@@ -48,6 +48,21 @@ def kat():
 
 
 @pytest.fixture(scope="session")
+def mesh_golden(tmp_path_factory):
+    """The edge-case mesh scene (BVH-sized: duplicates, a fan, triangles in
+    the back wall's plane; tests/golden/mesh_scene.py) and the reference's
+    render of it (gen_golden.py mesh): (scene, golden dict)."""
+    sys.path.insert(0, GOLDEN)
+    import mesh_scene as ms
+    from pathtracerpython_amd import scene_reader
+    scene_reader.VERBOSE = False
+    d = tmp_path_factory.mktemp("mesh_golden")
+    sc = scene_reader.Scene(ms.write_mesh_scene(str(d), os.path.dirname(CORNELL)))
+    g = np.load(os.path.join(GOLDEN, ms.NAME))
+    return sc, {k: g[k] for k in g.files}
+
+
+@pytest.fixture(scope="session")
 def hostcheck():
     """Host build of the kernel's per-lane code (tests/hostcheck)."""
     d = os.path.join(ROOT, "tests", "hostcheck")

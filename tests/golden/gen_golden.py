@@ -19,7 +19,7 @@ What it does (SURVEY.md §8c "Deterministic harness"):
     before min-max normalisation, and also keeps the real make_image output;
   * overrides the SDL `size` (scene_reader.py:153-155) via a Scene subclass.
 
-Usage:  python gen_golden.py [all|scene|kat|render W H SPP B SEED]
+Usage:  python gen_golden.py [all|scene|kat|mesh|render W H SPP B SEED]
 """
 import contextlib
 import io
@@ -133,8 +133,9 @@ def make_sync_pool(ref_main, rng):
     return SyncPool
 
 
-def render_reference(width, height, spp, bounces, seed):
-    """Run the unmodified reference main() under the keyed harness."""
+def render_reference(width, height, spp, bounces, seed, scene=None):
+    """Run the unmodified reference main() under the keyed harness (on
+    `scene`, an SDL path; default the reference's Cornell room)."""
     ref_main, ref_utils, ref_scene = import_reference()
     rng = KeyedRNG(seed, ref_main.main.__code__)
     ref_main.uniform = rng.uniform
@@ -160,7 +161,7 @@ def render_reference(width, height, spp, bounces, seed):
 
     ref_main.make_image = capture
     argv = sys.argv
-    sys.argv = ["main.py", SCENE, "-r", str(spp), "-b", str(bounces)]
+    sys.argv = ["main.py", scene or SCENE, "-r", str(spp), "-b", str(bounces)]
     try:
         with contextlib.redirect_stdout(io.StringIO()):
             ref_main.main()
@@ -176,6 +177,19 @@ def gen_render(width, height, spp, bounces, seed):
                         width=width, height=height, spp=spp, bounces=bounces,
                         seed=seed)
     print("wrote", name, colors.shape, float(colors.min()), float(colors.max()))
+
+
+def gen_mesh():
+    """The BVH golden: the reference on the edge-case mesh scene of
+    mesh_scene.py (written into a temporary directory)."""
+    import tempfile
+    import mesh_scene as ms
+    d = tempfile.mkdtemp(prefix="pt_mesh_")
+    sdl = ms.write_mesh_scene(d, os.path.join(REF, "objs"))
+    colors, png = render_reference(ms.W, ms.H, ms.SPP, ms.BOUNCES, ms.SEED, scene=sdl)
+    np.savez_compressed(os.path.join(HERE, ms.NAME), colors=colors, png=png, width=ms.W,
+                        height=ms.H, spp=ms.SPP, bounces=ms.BOUNCES, seed=ms.SEED)
+    print("wrote", ms.NAME, colors.shape, float(colors.min()), float(colors.max()))
 
 
 def gen_scene():
@@ -368,6 +382,8 @@ if __name__ == "__main__":
         gen_scene()
     if what in ("all", "kat"):
         gen_kat()
+    if what in ("all", "mesh"):
+        gen_mesh()
     if what == "render":
         gen_render(*[int(x) for x in sys.argv[2:7]])
     if what == "all":

@@ -67,6 +67,23 @@ def test_matches_oracle(R, packed, W, H, spp, B, seed, rr):
     assert np.abs(to_list_order(fb) - ref).max() <= TOL
 
 
+def test_mesh_golden(mesh_golden):
+    """The BVH path against the reference itself: the edge-case mesh scene
+    (68 triangles above the BVH threshold: duplicates, a shared-edge fan,
+    triangles in the back wall's plane; tests/golden/mesh_scene.py) through
+    the wavefront kernels (the default for BVH scenes) and the single kernel,
+    f64 and f32 framebuffers."""
+    sc, g = mesh_golden
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    with Renderer(sc) as r:
+        wf = r.render(W, H, spp, B, seed, out_f64=True)
+        mk = r.render(W, H, spp, B, seed, out_f64=True, megakernel=True)
+        f32 = r.render(W, H, spp, B, seed)
+    assert np.array_equal(wf, mk)
+    assert np.abs(to_list_order(wf) - g["colors"]).max() <= TOL
+    assert np.abs(to_list_order(f32) - g["colors"]).max() <= 1e-6
+
+
 def test_zero_bounces_is_black(R):
     assert not R.render(8, 8, 2, 0, 1).any()
 

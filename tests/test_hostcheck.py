@@ -242,6 +242,18 @@ def test_wavefront_equals_single_kernel_small_k5(hostcheck, tmp_path):
     _wavefront_case(hostcheck, pk, 8, 8, 1, 1, 3)                 # primary shading only
 
 
+def test_mesh_golden_bvh_and_wavefront(hostcheck, mesh_golden):
+    """The host build's BVH walks (forced f64 and hybrid) and its wavefront
+    state machine on the edge-case mesh scene, against the reference's render
+    of it (tests/golden/mesh_scene.py)."""
+    sc, g = mesh_golden
+    pk = pack_scene(sc)
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    _bvh_case(hostcheck, pk, W, H, spp, B, seed)
+    out = _wavefront_case(hostcheck, pk, W, H, spp, B, seed)
+    assert np.abs(to_list_order(out) - g["colors"]).max() <= 1e-12
+
+
 def test_wavefront_needs_a_bvh(hostcheck, packed):
     p = make_params(8, 8, 1, 2, 1)
     out = np.zeros((8, 8, 3))
