@@ -63,6 +63,22 @@ def mesh_golden(tmp_path_factory):
 
 
 @pytest.fixture(scope="session")
+def k5mini_golden(tmp_path_factory):
+    """The K5 scene generator at 1,000 triangles (synth.write_k5_scene, the
+    BASELINE config-5 distribution) and the reference's render of it
+    (gen_golden.py k5mini): (scene, golden dict)."""
+    from pathtracerpython_amd import scene_reader
+    from pathtracerpython_amd.synth import write_k5_scene
+    scene_reader.VERBOSE = False
+    g = np.load(os.path.join(GOLDEN, "k5mini_render_8x8_s2_b3_seed9.npz"))
+    g = {k: g[k] for k in g.files}
+    d = tmp_path_factory.mktemp("k5mini_golden")
+    sc = scene_reader.Scene(write_k5_scene(str(d), n_tris=int(g["n_tris"]), seed=0,
+                                           size=int(g["width"])))
+    return sc, g
+
+
+@pytest.fixture(scope="session")
 def hostcheck():
     """Host build of the kernel's per-lane code (tests/hostcheck)."""
     d = os.path.join(ROOT, "tests", "hostcheck")

@@ -19,7 +19,7 @@ What it does (SURVEY.md §8c "Deterministic harness"):
     before min-max normalisation, and also keeps the real make_image output;
   * overrides the SDL `size` (scene_reader.py:153-155) via a Scene subclass.
 
-Usage:  python gen_golden.py [all|scene|kat|mesh|render W H SPP B SEED]
+Usage:  python gen_golden.py [all|scene|kat|mesh|k5mini|render W H SPP B SEED]
 """
 import contextlib
 import io
@@ -190,6 +190,27 @@ def gen_mesh():
     np.savez_compressed(os.path.join(HERE, ms.NAME), colors=colors, png=png, width=ms.W,
                         height=ms.H, spp=ms.SPP, bounces=ms.BOUNCES, seed=ms.SEED)
     print("wrote", ms.NAME, colors.shape, float(colors.min()), float(colors.max()))
+
+
+K5MINI = dict(n_tris=1000, W=8, H=8, spp=2, bounces=3, seed=9)
+K5MINI_NAME = "k5mini_render_8x8_s2_b3_seed9.npz"   # (not render_*: the Cornell goldens)
+
+
+def gen_k5mini():
+    """The K5 scene generator (pathtracerpython_amd/synth.py, the BASELINE
+    config-5 distribution) at 1,000 triangles, rendered by the reference."""
+    import tempfile
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from pathtracerpython_amd.synth import write_k5_scene
+    c = K5MINI
+    d = tempfile.mkdtemp(prefix="pt_k5mini_")
+    sdl = write_k5_scene(d, n_tris=c["n_tris"], seed=0, size=c["W"],
+                         cornell_dir=os.path.join(REF, "objs"))
+    colors, png = render_reference(c["W"], c["H"], c["spp"], c["bounces"], c["seed"], scene=sdl)
+    np.savez_compressed(os.path.join(HERE, K5MINI_NAME), colors=colors, png=png, width=c["W"],
+                        height=c["H"], spp=c["spp"], bounces=c["bounces"], seed=c["seed"],
+                        n_tris=c["n_tris"])
+    print("wrote", K5MINI_NAME, colors.shape, float(colors.min()), float(colors.max()))
 
 
 def gen_scene():
@@ -384,6 +405,8 @@ if __name__ == "__main__":
         gen_kat()
     if what in ("all", "mesh"):
         gen_mesh()
+    if what in ("all", "k5mini"):
+        gen_k5mini()
     if what == "render":
         gen_render(*[int(x) for x in sys.argv[2:7]])
     if what == "all":

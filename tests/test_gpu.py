@@ -84,6 +84,20 @@ def test_mesh_golden(mesh_golden):
     assert np.abs(to_list_order(f32) - g["colors"]).max() <= 1e-6
 
 
+def test_k5mini_golden(k5mini_golden):
+    """The K5 scene generator at 1,000 triangles against the reference's
+    own render (wavefront and single kernel, f64 and f32 framebuffers)."""
+    sc, g = k5mini_golden
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    with Renderer(sc) as r:
+        wf = r.render(W, H, spp, B, seed, out_f64=True)
+        mk = r.render(W, H, spp, B, seed, out_f64=True, megakernel=True)
+        f32 = r.render(W, H, spp, B, seed)
+    assert np.array_equal(wf, mk)
+    assert np.abs(to_list_order(wf) - g["colors"]).max() <= TOL
+    assert np.abs(to_list_order(f32) - g["colors"]).max() <= 1e-6
+
+
 def test_zero_bounces_is_black(R):
     assert not R.render(8, 8, 2, 0, 1).any()
 

@@ -254,6 +254,17 @@ def test_mesh_golden_bvh_and_wavefront(hostcheck, mesh_golden):
     assert np.abs(to_list_order(out) - g["colors"]).max() <= 1e-12
 
 
+def test_k5mini_golden_bvh_and_wavefront(hostcheck, k5mini_golden):
+    """The host build's BVH walks and wavefront state machine on the K5
+    scene generator at 1,000 triangles, against the reference's render."""
+    sc, g = k5mini_golden
+    pk = pack_scene(sc)
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    _bvh_case(hostcheck, pk, W, H, spp, B, seed)
+    out = _wavefront_case(hostcheck, pk, W, H, spp, B, seed)
+    assert np.abs(to_list_order(out) - g["colors"]).max() <= 1e-12
+
+
 def test_wavefront_needs_a_bvh(hostcheck, packed):
     p = make_params(8, 8, 1, 2, 1)
     out = np.zeros((8, 8, 3))

@@ -138,3 +138,13 @@ def test_oracle_matches_mesh_golden(mesh_golden):
     W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
     ref, _ = oracle.render(pack_scene(sc), W, H, spp, B, seed)
     assert np.abs(ref - g["colors"]).max() <= 1e-12
+
+
+def test_oracle_matches_k5mini_golden(k5mini_golden):
+    """The K5 scene generator at 1,000 triangles: the oracle against the
+    reference's own render (gen_golden.py k5mini)."""
+    from pathtracerpython_amd.pack import pack_scene
+    sc, g = k5mini_golden
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    ref, _ = oracle.render(pack_scene(sc), W, H, spp, B, seed)
+    assert np.abs(ref - g["colors"]).max() <= 1e-12
