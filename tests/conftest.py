@@ -78,6 +78,25 @@ def k5mini_golden(tmp_path_factory):
     return sc, g
 
 
+def scene_goldens():
+    """The reference's renders of the test scenes below (gen_golden.py
+    scenes): [(name, writer, golden dict)]."""
+    out = []
+    for f in sorted(glob.glob(os.path.join(GOLDEN, "*_scene_*_render_*.npz"))):
+        g = np.load(f)
+        name = os.path.basename(f)
+        out.append((name, name.split("_render_")[0].rsplit("_", 1)[0], {k: g[k] for k in g.files}))
+    return out
+
+
+def scene_golden_ids():
+    return [n for n, _, _ in scene_goldens()]
+
+
+def scene_of_golden(tmp_path, writer, g):
+    return globals()[writer](tmp_path, int(g["scene_seed"]))
+
+
 @pytest.fixture(scope="session")
 def hostcheck():
     """Host build of the kernel's per-lane code (tests/hostcheck)."""

@@ -19,7 +19,7 @@ What it does (SURVEY.md §8c "Deterministic harness"):
     before min-max normalisation, and also keeps the real make_image output;
   * overrides the SDL `size` (scene_reader.py:153-155) via a Scene subclass.
 
-Usage:  python gen_golden.py [all|scene|kat|mesh|k5mini|render W H SPP B SEED]
+Usage:  python gen_golden.py [all|scene|kat|mesh|k5mini|scenes|render W H SPP B SEED]
 """
 import contextlib
 import io
@@ -211,6 +211,35 @@ def gen_k5mini():
                         height=c["H"], spp=c["spp"], bounces=c["bounces"], seed=c["seed"],
                         n_tris=c["n_tris"])
     print("wrote", K5MINI_NAME, colors.shape, float(colors.min()), float(colors.max()))
+
+
+# goldens of the test scenes built by tests/conftest.py (same writers, same
+# seeds): (writer, scene seed, W, H, spp, bounces, render seed)
+SCENE_GOLDENS = [
+    ("quad_scene", 3, 12, 12, 3, 4, 3),         # parallelogram units (pt_path.h quad_m)
+    ("multi_mesh_scene", 3, 10, 10, 2, 3, 3),   # two BVH objects first in scene order
+]
+
+
+def scene_golden_name(writer, sseed, W, H, spp, B, seed):
+    return f"{writer}_{sseed}_render_{W}x{H}_s{spp}_b{B}_seed{seed}.npz"
+
+
+def gen_scene_goldens():
+    """The reference on the test scenes of tests/conftest.py (written into a
+    temporary directory by the writers the tests use)."""
+    import pathlib
+    import tempfile
+    sys.path.insert(0, os.path.dirname(HERE))
+    import conftest
+    for writer, sseed, W, H, spp, B, seed in SCENE_GOLDENS:
+        d = pathlib.Path(tempfile.mkdtemp(prefix="pt_scene_"))
+        getattr(conftest, writer)(d, sseed)
+        colors, png = render_reference(W, H, spp, B, seed, scene=str(d / "scene.sdl"))
+        name = scene_golden_name(writer, sseed, W, H, spp, B, seed)
+        np.savez_compressed(os.path.join(HERE, name), colors=colors, png=png, width=W, height=H,
+                            spp=spp, bounces=B, seed=seed, scene_seed=sseed)
+        print("wrote", name, colors.shape, float(colors.min()), float(colors.max()))
 
 
 def gen_scene():
@@ -407,6 +436,8 @@ if __name__ == "__main__":
         gen_mesh()
     if what in ("all", "k5mini"):
         gen_k5mini()
+    if what in ("all", "scenes"):
+        gen_scene_goldens()
     if what == "render":
         gen_render(*[int(x) for x in sys.argv[2:7]])
     if what == "all":

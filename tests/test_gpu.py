@@ -10,7 +10,8 @@ determinism) cover the whole image."""
 import numpy as np
 import pytest
 
-from conftest import golden_renders, multi_mesh_scene, quad_scene, random_scene
+from conftest import (golden_renders, multi_mesh_scene, quad_scene, random_scene, scene_golden_ids,
+                      scene_goldens, scene_of_golden)
 from oracle import oracle
 from pathtracerpython_amd import _native
 from pathtracerpython_amd.pack import pack_scene
@@ -95,6 +96,22 @@ def test_k5mini_golden(k5mini_golden):
         f32 = r.render(W, H, spp, B, seed)
     assert np.array_equal(wf, mk)
     assert np.abs(to_list_order(wf) - g["colors"]).max() <= TOL
+    assert np.abs(to_list_order(f32) - g["colors"]).max() <= 1e-6
+
+
+@pytest.mark.parametrize("name,writer,g", scene_goldens(), ids=scene_golden_ids())
+def test_scene_goldens(tmp_path, name, writer, g):
+    """The quad-unit and two-mesh test scenes against the reference's own
+    renders (gen_golden.py scenes): default path (wavefront for the BVH
+    scene), single kernel, forced f64, f32 framebuffer."""
+    sc = scene_of_golden(tmp_path, writer, g)
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    with Renderer(sc) as r:
+        fb = r.render(W, H, spp, B, seed, out_f64=True)
+        assert np.array_equal(fb, r.render(W, H, spp, B, seed, out_f64=True, megakernel=True))
+        assert np.array_equal(fb, r.render(W, H, spp, B, seed, out_f64=True, force_f64=True))
+        f32 = r.render(W, H, spp, B, seed)
+    assert np.abs(to_list_order(fb) - g["colors"]).max() <= TOL
     assert np.abs(to_list_order(f32) - g["colors"]).max() <= 1e-6
 
 

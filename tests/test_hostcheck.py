@@ -8,7 +8,8 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from conftest import golden_renders, hc_render, multi_mesh_scene, quad_scene, random_scene
+from conftest import (golden_renders, hc_render, multi_mesh_scene, quad_scene, random_scene,
+                      scene_golden_ids, scene_goldens, scene_of_golden)
 from oracle import oracle
 from pathtracerpython_amd._abi import PT_FLAG_RR, make_params
 from pathtracerpython_amd.pack import pack_scene
@@ -263,6 +264,22 @@ def test_k5mini_golden_bvh_and_wavefront(hostcheck, k5mini_golden):
     _bvh_case(hostcheck, pk, W, H, spp, B, seed)
     out = _wavefront_case(hostcheck, pk, W, H, spp, B, seed)
     assert np.abs(to_list_order(out) - g["colors"]).max() <= 1e-12
+
+
+@pytest.mark.parametrize("name,writer,g", scene_goldens(), ids=scene_golden_ids())
+def test_scene_goldens_host(hostcheck, tmp_path, name, writer, g):
+    """The host build (hybrid and forced f64; the wavefront state machine
+    where the scene has a BVH) on the quad and two-mesh test scenes, against
+    the reference's renders of them."""
+    pk = pack_scene(scene_of_golden(tmp_path, writer, g))
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    p = make_params(W, H, spp, B, seed)
+    a, _ = hc_render(hostcheck, pk, p, False, count=False)
+    b, _ = hc_render(hostcheck, pk, p, True, count=False)
+    assert np.array_equal(a, b)
+    assert np.abs(to_list_order(a) - g["colors"]).max() <= 1e-12
+    if writer == "multi_mesh_scene":
+        assert np.array_equal(_wavefront_case(hostcheck, pk, W, H, spp, B, seed), a)
 
 
 def test_wavefront_needs_a_bvh(hostcheck, packed):

@@ -7,7 +7,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden_renders
+from conftest import GOLDEN, golden_renders, scene_golden_ids, scene_goldens, scene_of_golden
 
 sys.path.insert(0, GOLDEN)
 from philox_ref import keyed_u, philox4x32_10  # noqa: E402
@@ -147,4 +147,15 @@ def test_oracle_matches_k5mini_golden(k5mini_golden):
     sc, g = k5mini_golden
     W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
     ref, _ = oracle.render(pack_scene(sc), W, H, spp, B, seed)
+    assert np.abs(ref - g["colors"]).max() <= 1e-12
+
+
+@pytest.mark.parametrize("name,writer,g", scene_goldens(), ids=scene_golden_ids())
+def test_oracle_matches_scene_goldens(tmp_path, name, writer, g):
+    """The test scenes with parallelogram units (quad_scene) and two BVH
+    objects first in scene order (multi_mesh_scene): the oracle against the
+    reference's own renders (gen_golden.py scenes)."""
+    from pathtracerpython_amd.pack import pack_scene
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    ref, _ = oracle.render(pack_scene(scene_of_golden(tmp_path, writer, g)), W, H, spp, B, seed)
     assert np.abs(ref - g["colors"]).max() <= 1e-12
