@@ -424,6 +424,7 @@ RENDER_CONFIGS = [
     (64, 64, 1, 1, 9),      # BASELINE config 1 (-b 1 is main.py's default)
     (64, 64, 1, 4, 9),
     (24, 24, 3, 5, 12345),
+    (6, 6, 32, 3, 21),      # several lanes per pixel on the GPU (split 4, xor-ordered sums)
 ]
 
 if __name__ == "__main__":
