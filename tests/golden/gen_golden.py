@@ -19,7 +19,7 @@ What it does (SURVEY.md §8c "Deterministic harness"):
     before min-max normalisation, and also keeps the real make_image output;
   * overrides the SDL `size` (scene_reader.py:153-155) via a Scene subclass.
 
-Usage:  python gen_golden.py [all|scene|kat|mesh|k5mini|scenes|render W H SPP B SEED]
+Usage:  python gen_golden.py [all|scene|kat|mesh|meshkat|k5mini|scenes|render W H SPP B SEED]
 """
 import contextlib
 import io
@@ -190,6 +190,49 @@ def gen_mesh():
     np.savez_compressed(os.path.join(HERE, ms.NAME), colors=colors, png=png, width=ms.W,
                         height=ms.H, spp=ms.SPP, bounces=ms.BOUNCES, seed=ms.SEED)
     print("wrote", ms.NAME, colors.shape, float(colors.min()), float(colors.max()))
+
+
+def gen_mesh_kat():
+    """`intersect_objects` (main.py:83-122) of the reference on the edge-case
+    mesh scene (mesh_scene.py): the batched closest-hit API over a BVH object,
+    with origins in the room, on the mesh's triangles (the sqd > 1e-5
+    self-hit rule; duplicates) and at the eye."""
+    import tempfile
+    import mesh_scene as ms
+    ref_main, _, ref_scene = import_reference()
+    d = tempfile.mkdtemp(prefix="pt_mesh_kat_")
+    sdl = ms.write_mesh_scene(d, os.path.join(REF, "objs"))
+    with contextlib.redirect_stdout(io.StringIO()):
+        sc = ref_scene.Scene(sdl)
+    rs = np.random.RandomState(4321)
+    mesh = ms.mesh_triangles()
+    objs_plus = sc.objects + [{"geometry": sc.light_obj}]
+    io_o, io_d, io_hit, io_p, io_obj, io_light = [], [], [], [], [], []
+    for k in range(400):
+        if k % 4 == 0:
+            o = np.array(sc.eye, dtype=np.float64)
+            dd = np.array([rs.uniform(-1, 1), rs.uniform(-1, 1), 0.0]) - o
+        elif k % 4 == 1:   # on a mesh triangle (its centroid)
+            t = mesh[rs.randint(len(mesh))]
+            o = (t[0] + t[1] + t[2]) / 3.0
+            dd = rs.normal(0, 1, 3)
+        else:
+            o = rs.uniform([-3.8, -3.8, -32.7], [3.8, 3.8, -16.6])
+            dd = rs.normal(0, 1, 3)
+        r = ref_main.intersect_objects((o, dd), sc.objects, sc.light_obj)
+        io_o.append(o); io_d.append(dd)
+        if r is None:
+            io_hit.append(0); io_p.append(np.zeros(3)); io_obj.append(-1); io_light.append(0)
+        else:
+            p, n, obj, is_light = r
+            idx = [i for i, oo in enumerate(objs_plus) if oo["geometry"] is obj["geometry"]][0]
+            io_hit.append(1); io_p.append(np.asarray(p, dtype=np.float64))
+            io_obj.append(idx); io_light.append(int(is_light))
+    np.savez_compressed(os.path.join(HERE, "kat_mesh.npz"), io_o=np.array(io_o),
+                        io_d=np.array(io_d), io_hit=np.array(io_hit, dtype=np.int32),
+                        io_p=np.array(io_p), io_obj=np.array(io_obj, dtype=np.int32),
+                        io_light=np.array(io_light, dtype=np.int32))
+    print("wrote kat_mesh.npz", int(np.sum(io_hit)), "hits of", len(io_hit))
 
 
 K5MINI = dict(n_tris=1000, W=8, H=8, spp=2, bounces=3, seed=9)
@@ -435,6 +478,9 @@ if __name__ == "__main__":
         gen_kat()
     if what in ("all", "mesh"):
         gen_mesh()
+        gen_mesh_kat()
+    if what == "meshkat":
+        gen_mesh_kat()
     if what in ("all", "k5mini"):
         gen_k5mini()
     if what in ("all", "scenes"):
