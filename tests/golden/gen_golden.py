@@ -228,10 +228,34 @@ def gen_mesh_kat():
             idx = [i for i, oo in enumerate(objs_plus) if oo["geometry"] is obj["geometry"]][0]
             io_hit.append(1); io_p.append(np.asarray(p, dtype=np.float64))
             io_obj.append(idx); io_light.append(int(is_light))
+    # compute_color (main.py:23-80, 142-145) at points on every object's
+    # triangles, the mesh's included: shadow rays against the BVH object and
+    # the leaked colour of the last one across BVH and uniform occluders
+    rng = KeyedRNG(0, None)
+    ref_main.uniform = rng.uniform
+    import utils as ref_utils   # (already imported by import_reference)
+    ref_utils.uniform = rng.uniform
+    cc_p, cc_n, cc_obj, cc_u, cc_out = [], [], [], [], []
+    for k in range(300):
+        oi = rs.randint(len(sc.objects))
+        g = sc.objects[oi]["geometry"]
+        ti = rs.randint(len(g.triangles))
+        t = np.array([list(v) for v in g.triangles[ti]])
+        p = rs.dirichlet([1, 1, 1]) @ t
+        n = g.normals[ti]
+        u12 = [float(x) for x in rs.uniform(0, 1, 12)]
+        rng.forced = list(u12)
+        col = ref_main.compute_color(sc, sc.objects[oi], p, n)
+        assert not rng.forced
+        cc_p.append(p); cc_n.append(list(n)); cc_obj.append(oi)
+        cc_u.append(u12); cc_out.append(np.asarray(col, dtype=np.float64))
     np.savez_compressed(os.path.join(HERE, "kat_mesh.npz"), io_o=np.array(io_o),
                         io_d=np.array(io_d), io_hit=np.array(io_hit, dtype=np.int32),
                         io_p=np.array(io_p), io_obj=np.array(io_obj, dtype=np.int32),
-                        io_light=np.array(io_light, dtype=np.int32))
+                        io_light=np.array(io_light, dtype=np.int32),
+                        cc_p=np.array(cc_p), cc_n=np.array(cc_n),
+                        cc_obj=np.array(cc_obj, dtype=np.int32), cc_u=np.array(cc_u),
+                        cc_out=np.array(cc_out))
     print("wrote kat_mesh.npz", int(np.sum(io_hit)), "hits of", len(io_hit))
 
 

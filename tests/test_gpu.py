@@ -317,6 +317,19 @@ def test_mesh_kat_intersect_objects(mesh_golden):
     assert np.abs(P[hit] - k["io_p"][hit]).max() <= 1e-11
 
 
+def test_mesh_kat_compute_color(mesh_golden):
+    """The batched shading API over a scene with a BVH object
+    (pt_compute_color: shadow rays through the BVH walks) against the
+    reference's compute_color on the edge-case mesh scene."""
+    import os
+    from conftest import GOLDEN
+    sc, _ = mesh_golden
+    k = np.load(os.path.join(GOLDEN, "kat_mesh.npz"))
+    with Renderer(sc) as r:
+        out = r.compute_color(k["cc_obj"], k["cc_p"], k["cc_n"], k["cc_u"])
+    assert np.abs(out - k["cc_out"]).max() <= TOL
+
+
 def test_intersect_objects_outside_box(R, packed):
     rs = np.random.RandomState(0)
     o = rs.uniform(-100, 100, (500, 3))

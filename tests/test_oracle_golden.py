@@ -175,3 +175,14 @@ def test_mesh_kat_intersect_objects(mesh_golden):
     assert np.array_equal(np.where(hit, pk.tri_obj[np.maximum(tri, 0)], -1), k["io_obj"])
     assert np.array_equal((tri >= pk.n_obj_tri).astype(np.int32), k["io_light"])
     assert np.abs(P[hit] - k["io_p"][hit]).max() <= 1e-11
+
+
+def test_mesh_kat_compute_color(mesh_golden):
+    """compute_color of the reference at points on every object of the
+    edge-case mesh scene (shadow rays against the BVH object, the leaked
+    colour across BVH and uniform occluders), against the oracle."""
+    from pathtracerpython_amd.pack import pack_scene
+    sc, _ = mesh_golden
+    k = np.load(os.path.join(GOLDEN, "kat_mesh.npz"))
+    out = oracle.compute_color(pack_scene(sc), k["cc_obj"], k["cc_p"], k["cc_n"], k["cc_u"])
+    assert np.abs(out - k["cc_out"]).max() <= 1e-12
