@@ -39,6 +39,19 @@ def test_device_image_matches_reference_png(R, name, g):
     assert np.array_equal(image_u8(fb), g["png"])
 
 
+@pytest.mark.parametrize("which", ["mesh", "k5mini"])
+def test_device_image_matches_reference_png_bvh(mesh_golden, k5mini_golden, which):
+    """The BVH scenes' images (the edge-case mesh, the K5 generator at 1,000
+    triangles): rendered and finalised on the device, bit-exact against the
+    reference's make_image output of its own render."""
+    sc, g = mesh_golden if which == "mesh" else k5mini_golden
+    W, H, spp, B, seed = (int(g[k]) for k in ("width", "height", "spp", "bounces", "seed"))
+    with Renderer(sc) as r:
+        img, fb = r.render_image(W, H, spp, B, seed, return_fb=True)
+    assert np.array_equal(img, g["png"]), which
+    assert np.array_equal(image_u8(fb), g["png"])
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("shape", [(1, 1), (7, 3), (64, 64), (509, 1031)])
 def test_image_u8_matches_numpy(dtype, shape):
