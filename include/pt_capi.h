@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 2
+#define PT_API_VERSION 3
 
 /* error codes */
 #define PT_OK 0
@@ -162,7 +162,8 @@ int pt_render(pt_scene* scene, const pt_render_params* p, void* out_rgb_host,
  * of out_rgb_host ((row_end-row_begin) x width x 3, the layout pt_render
  * writes for the whole range).  Bit-identical to pt_render of the same range
  * on one device.  Synchronous.  stats (optional) receives the per-device sums
- * (PT_FLAG_COUNT renders then run one device at a time). */
+ * of every field (PT_FLAG_COUNT / PT_FLAG_WALK_COUNT / PT_FLAG_KERNEL_TIMES
+ * renders then run one device at a time). */
 int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* p,
                     void* out_rgb_host, pt_stats* stats);
 
@@ -183,6 +184,18 @@ int pt_intersect_objects(pt_scene* scene, const double* rays, int64_t n,
 int pt_compute_color(pt_scene* scene, const int32_t* obj, const double* point,
                      const double* normal, const double* u, int64_t n,
                      double* out_rgb);
+
+/* Frame assembly after the multi-GPU gather (replaces the
+ * reference's collection of Pool results, main.py:224-231): tiles_dev is the
+ * gathered (world, max_rows, width, 3) array whose band r is what
+ * pt_render_device writes for row_step = world, row_phase = r over the whole
+ * image (rows iy % world == r, top-first; max_rows >= ceil(height / world));
+ * out_dev receives the (height, width, 3) framebuffer in image orientation.
+ * Elements are float32, or float64 with PT_FLAG_OUT_F64 in flags.
+ * Asynchronous on `stream`. */
+int pt_assemble_bands_device(const void* tiles_dev, int32_t world, int32_t max_rows,
+                             int32_t width, int32_t height, uint32_t flags, void* out_dev,
+                             void* stream);
 
 /* Image finalisation of make_image (utils.py:150-161) on the device:
  * global min over the whole height x width x 3 array, shift, divide by the

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pt_capi.h (structs, flags, error codes)."""
 import ctypes as C
 
-PT_API_VERSION = 2
+PT_API_VERSION = 3
 
 PT_OK = 0
 PT_EINVAL = -1

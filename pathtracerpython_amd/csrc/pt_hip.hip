@@ -245,7 +245,8 @@ __device__ __forceinline__ void wf_append3(uint32_t want, int32_t* counter, int3
 #define PT_SHADE_BLOCK 256
 #endif
 constexpr int kShadeBlock = PT_SHADE_BLOCK;
-static_assert(kShadeBlock % 64 == 0 && kShadeBlock <= 1024, "whole waves");
+// (>= 128: wf_append_block issues its two list atomics from waves 0 and 1)
+static_assert(kShadeBlock % 64 == 0 && kShadeBlock >= 128 && kShadeBlock <= 1024, "whole waves, >= 2");
 __device__ __forceinline__ void wf_append_block(uint32_t want, int32_t* counters, int32_t* shadow_list,
                                                 int32_t* closest_list, int32_t slot) {
     constexpr int kWaves = kShadeBlock / 64;
@@ -587,8 +588,12 @@ __global__ __launch_bounds__(256) void k_intersect(SceneK S, const double* __res
     const bool in_a = in_box(to_f3(o - ld3(S.center)), xa);
     D3 P = d3(0, 0, 0);
     Counters c;
-    const int t = (in_s || in_a) ? closest<false, false>(S, o, d, -1, sp, &P, &c, !in_s)
-                                 : closest<true, false>(S, o, d, -1, sp, &P, &c, true);
+    // the uniform units take either frame (eye = !in_s), but the BVH walk
+    // always runs in the frame with the eye (its boxes' inflation assumes
+    // |o - center| <= xa): scenes with a BVH need in_a for the filter
+    const bool fast = S.n_bnode > 0 ? in_a : (in_s || in_a);
+    const int t = fast ? closest<false, false>(S, o, d, -1, sp, &P, &c, !in_s)
+                       : closest<true, false>(S, o, d, -1, sp, &P, &c, true);
     out_tri[i] = t;
     out_p[3 * i] = P.x; out_p[3 * i + 1] = P.y; out_p[3 * i + 2] = P.z;
 }
@@ -811,36 +816,57 @@ static int validate(const pt_render_params* p) {
     return PT_OK;
 }
 
-// Lanes (wavefront: path slots) per pixel: a power of two <= min(64, spp),
-// a function of the FULL image (width x height) and spp only — never of the
-// band a launch renders — so every band of an interleaved multi-GPU split
-// runs each pixel on the same lanes, sums its samples in the same order and
-// the bands assemble to the 1-GPU frame bit for bit.
+// Lanes (wavefront: path slots) per pixel: a power of two <= min(64, spp).
 //
-// Single kernel: >= 8 samples per lane, at most 2^30 lanes over the full
-// image (K2 512^2 x 64 spp: 8 lanes per pixel; K3 and K4: 64).
+// Single kernel (scenes without a BVH): >= 8 samples per lane where the
+// launch is large (K2 512^2 x 64 spp: 8 lanes per pixel; K3 and K4: 64), at
+// most 2^30 lanes over the full image — but at least `min_lanes` lanes in the
+// launch, i.e. ~4 dispatch rounds of the device's resident waves (n_cu x 4
+// SIMDs x 4 waves x 64 lanes x 4 rounds = 2^20 on MI355X).  A launch of one
+// round is as long as its slowest wave (~0.7 ms at K2) however little work
+// the band holds: one rank's band of an N-GPU strong-scaling split of the K2
+// frame, per-band kernel ms at 8 / 16 / 32 / 64 lanes per
+// pixel: N=4 1.592 / 1.450 / 1.480 / 1.566, N=8 0.882 / 0.816 / 0.767 / 0.809
+// (N=1 5.584 / 5.674 / 5.792 / 6.136: each lane traces its pixel's primary
+// ray once).  A pixel's samples are summed in an order that depends on its
+// lane count, so bands of different sizes round differently in the last
+// bits (all within 1e-12 of the oracle); bands of equal launch size agree bit
+// for bit.
 // Wavefront (BVH scenes): path slots hold ~420 B of state each, so at most
 // 64M slots (28 GB) over the full image (K5 512^2 x 64 spp: 2M slots 161.6
 // ms, 4M 147.1, 8M 140.5, 16M 139.3 (round 1); 1024^2 x 256 spp with the
 // one-ray walks: 16M 1419 ms, 32M 1392, 64M 1378 — fewer shade / walk steps,
-// each with its drain); an N-way band gets 1/N of them.  The single kernel uses the same split on BVH
-// scenes, so its framebuffer stays bitwise equal to the wavefront one.
+// each with its drain); an N-way band gets 1/N of them.  The single kernel
+// uses the same split on BVH scenes (min_lanes does not apply), so its
+// framebuffer stays bitwise equal to the wavefront one.
 //
 // PT_SPLIT_FIXED (compile-time, tuning builds only) pins the split.
-static uint32_t choose_split(uint64_t image_pixels, int32_t spp, bool bvh) {
+static uint32_t choose_split(uint64_t image_pixels, uint64_t launch_pixels, int32_t spp, bool bvh,
+                             uint64_t min_lanes) {
     uint32_t cap = 64;
     while (cap > 1 && (int32_t)cap > spp) cap >>= 1;
 #ifdef PT_SPLIT_FIXED
     uint32_t f = 1;
     while (f * 2 <= (uint32_t)PT_SPLIT_FIXED && f * 2 <= cap) f *= 2;
-    (void)image_pixels; (void)bvh;
+    (void)image_pixels; (void)launch_pixels; (void)bvh; (void)min_lanes;
     return f;
 #else
     uint32_t s = 1;
     const uint64_t target = (uint64_t)1 << (bvh ? 26 : 30);
     while (s < cap && image_pixels * s * 2 <= target && (bvh || spp / (int32_t)(s * 2) >= 8)) s *= 2;
+    if (!bvh)
+        while (s < cap && launch_pixels * s < min_lanes) s *= 2;
     return s;
 #endif
+}
+// lanes of a single-kernel launch below which it gets more lanes per pixel:
+// PT_MIN_ROUNDS dispatch rounds of the device's resident waves (4 per SIMD,
+// k_render's __launch_bounds__)
+#ifndef PT_MIN_ROUNDS
+#define PT_MIN_ROUNDS 4
+#endif
+static uint64_t min_lanes_of(int n_cu) {
+    return (uint64_t)n_cu * 4u * (uint64_t)PT_RENDER_WAVES * 64u * (uint64_t)PT_MIN_ROUNDS;
 }
 
 // Walk kernels: node-phase exit threshold (lanes still descending) and
@@ -1042,7 +1068,8 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     R.sample_begin = p->sample_begin;
     R.out_f64 = (p->flags & PT_FLAG_OUT_F64) ? 1 : 0;
     R.npix = (uint32_t)rows * (uint32_t)p->width;
-    R.split = choose_split((uint64_t)p->width * (uint64_t)p->height, p->spp, s->dev.n_bnode > 0);
+    R.split = choose_split((uint64_t)p->width * (uint64_t)p->height, (uint64_t)R.npix, p->spp,
+                           s->dev.n_bnode > 0, min_lanes_of(s->n_cu));
     R.split_log2 = 0;
     while ((1u << R.split_log2) < R.split) ++R.split_log2;
     R.tail_pix = R.npix;
@@ -1055,8 +1082,6 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
         // interleaved band) gets 8x the lanes per pixel, so the last dispatch
         // round is short waves.  K2 6.70 -> 6.49 ms; sixteenth / eighth /
         // quarter of the rows at 2x / 4x / 8x lanes all land within 6.49-6.54.
-        // A pixel's lanes depend only on (iy, W, H, spp), so band renders
-        // still assemble bit for bit.
 #ifndef PT_TAIL_FRAC
 #define PT_TAIL_FRAC 16
 #endif
@@ -1071,11 +1096,10 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
         const int32_t thresh = p->height - (p->height + kTailFrac - 1) / kTailFrac;
         int32_t ra = 0;   // band rows below the threshold (a prefix: rows ascend)
         while (ra < rows && first + ra * p->row_step < thresh) ++ra;
-        // (no tail when the full image's lanes would overflow the 32-bit
-        // lane index: decided on the full image so bands still agree)
-        const uint64_t full_lanes = (uint64_t)thresh * p->width * R.split + 64 +
-                                    (((uint64_t)(p->height - thresh) * (uint64_t)p->width) << tl);
-        if (tl > R.split_log2 && ra < rows && full_lanes < ((uint64_t)1 << 32)) {
+        // (no tail when this launch's lanes would overflow the 32-bit lane index)
+        const uint64_t lanes = (uint64_t)ra * p->width * R.split + 64 +
+                               (((uint64_t)(rows - ra) * (uint64_t)p->width) << tl);
+        if (tl > R.split_log2 && ra < rows && lanes < ((uint64_t)1 << 32)) {
             R.tail_pix = (uint32_t)ra * (uint32_t)p->width;
             R.tail_lane = (R.tail_pix * R.split + 63u) & ~63u;
             R.tail_log2 = tl;
@@ -1159,6 +1183,24 @@ int pt_render(pt_scene* s, const pt_render_params* p, void* out_host, pt_stats* 
     return PT_OK;
 }
 
+}  // extern "C"
+
+static void add_stats(pt_stats* d, const pt_stats& s) {
+    d->closest_tests += s.closest_tests; d->shadow_tests += s.shadow_tests;
+    d->ray_bounces += s.ray_bounces; d->shading_points += s.shading_points;
+    d->light_hits += s.light_hits; d->escapes += s.escapes;
+    d->f64_fallbacks += s.f64_fallbacks; d->f64_rescans += s.f64_rescans;
+    d->shadow_queries += s.shadow_queries; d->shadow_node_visits += s.shadow_node_visits;
+    d->shadow_leaf_units += s.shadow_leaf_units; d->closest_queries += s.closest_queries;
+    d->closest_node_visits += s.closest_node_visits; d->closest_leaf_units += s.closest_leaf_units;
+    d->shade_ms += s.shade_ms; d->shadow_ms += s.shadow_ms; d->closest_ms += s.closest_ms;
+    d->shade_launches += s.shade_launches; d->shadow_launches += s.shadow_launches;
+    d->closest_launches += s.closest_launches;
+}
+static_assert(sizeof(pt_stats) == 17 * 8 + 3 * 8, "add_stats covers every pt_stats field");
+
+extern "C" {
+
 int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* p, void* out_host,
                     pt_stats* stats) {
     if (!scenes || n <= 0) return fail(PT_EINVAL, "need n >= 1 scene handles");
@@ -1174,7 +1216,9 @@ int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* 
     const int32_t rb = first, re = first + total;   // the rows, clamped to the image
     const size_t elem = (p->flags & PT_FLAG_OUT_F64) ? sizeof(double) : sizeof(float);
     const size_t row_bytes = (size_t)p->width * 3 * elem;
-    const bool count = (p->flags & PT_FLAG_COUNT) != 0;
+    // any stats-producing flag: every device's pt_stats is summed field by
+    // field (counts and the kernel-time sums alike)
+    const bool count = (p->flags & (PT_FLAG_COUNT | PT_FLAG_WALK_COUNT | PT_FLAG_KERNEL_TIMES)) != 0;
     if (stats) memset(stats, 0, sizeof(*stats));
     std::vector<pt_render_params> bp(n);
     std::vector<int32_t> rows(n, 0);
@@ -1201,11 +1245,7 @@ int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* 
         pt_stats st;
         rc = pt_render_device(s, &bp[i], s->out_dev, s->stream, (count && stats) ? &st : nullptr);
         if (rc) return rc;
-        if (count && stats) {
-            uint64_t* dst = &stats->closest_tests;
-            const uint64_t* src = &st.closest_tests;
-            for (int k = 0; k < 8; ++k) dst[k] += src[k];
-        }
+        if (count && stats) add_stats(stats, st);
     }
     // 2. each band lands in its rows of the host frame: band row j (launch
     // order, highest iy first) is frame row (re-1-iy) = (re-1-iy_top) + j*n
@@ -1261,6 +1301,28 @@ int pt_image_u8_device(const void* fb_dev, int32_t width, int32_t height, uint32
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipFreeAsync(keys, st));
+    return PT_OK;
+}
+
+int pt_assemble_bands_device(const void* tiles_dev, int32_t world, int32_t max_rows, int32_t width,
+                             int32_t height, uint32_t flags, void* out_dev, void* stream) {
+    if (!tiles_dev || !out_dev) return fail(PT_EINVAL, "null buffer");
+    if (world <= 0 || width <= 0 || height <= 0) return fail(PT_EINVAL, "need world, width, height > 0");
+    if (max_rows < (height + world - 1) / world)
+        return fail(PT_EINVAL, "max_rows is smaller than the largest band (ceil(height / world))");
+    const int64_t row_bytes = (int64_t)width * 3 * ((flags & PT_FLAG_OUT_F64) ? 8 : 4);
+    const bool v16 = row_bytes % 16 == 0 && (uintptr_t)tiles_dev % 16 == 0 && (uintptr_t)out_dev % 16 == 0;
+    const int64_t units = row_bytes / (v16 ? 16 : 4);
+    const int64_t n = (int64_t)height * units;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    if (v16)
+        hipLaunchKernelGGL(k_assemble_bands<uint4>, grid, block, 0, st, (const uint4*)tiles_dev, world, max_rows,
+                           height, units, (uint4*)out_dev);
+    else
+        hipLaunchKernelGGL(k_assemble_bands<uint32_t>, grid, block, 0, st, (const uint32_t*)tiles_dev, world,
+                           max_rows, height, units, (uint32_t*)out_dev);
+    HIPCHK(hipGetLastError());
     return PT_OK;
 }
 

@@ -125,4 +125,26 @@ __global__ __launch_bounds__(256) void k_to_u8(const T* __restrict__ fb, int64_t
         out[i] = (uint8_t)to_u8(load_f64(fb, i), mn, mx, nan);
 }
 
+// Frame assembly of an interleaved multi-GPU render (the step after the
+// RCCL gather): tiles = the gathered (world, max_rows, row)
+// array, band r holding the image rows iy % world == r top-first (as
+// pt_render_device writes a band); out = the (height, row) frame, row
+// height-1-iy holding image row iy.  One work-item per V-sized piece of an
+// output row (V = 16 B when every row offset is 16-B aligned, else 4 B):
+// HBM-bound, one read and one write of the frame.
+template <typename V>
+__global__ __launch_bounds__(256) void k_assemble_bands(const V* __restrict__ tiles, int32_t world,
+                                                        int32_t max_rows, int32_t height,
+                                                        int64_t row_units, V* __restrict__ out) {
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= (int64_t)height * row_units) return;
+    const int32_t fr = (int32_t)(gid / row_units);
+    const int64_t c = gid - (int64_t)fr * row_units;
+    const int32_t iy = height - 1 - fr;
+    const int32_t r = iy % world, k = iy / world;
+    const int32_t rows_r = (height - r + world - 1) / world;
+    const int32_t j = rows_r - 1 - k;   // band row, top-first
+    out[gid] = tiles[((int64_t)r * max_rows + j) * row_units + c];
+}
+
 }  // namespace pt

@@ -68,6 +68,33 @@ def deinterleave(gathered, out):
     return out
 
 
+def assemble_bands_device(gathered, out, stream=None):
+    """The frame from the gathered row tiles of an interleaved split, on the
+    GPU (pt_assemble_bands_device, one HBM-bound kernel; any height, also
+    ragged bands): gathered (world, max_rows, W, 3) float32/float64 device
+    tensor, out (H, W, 3) of the same dtype.  Asynchronous on `stream` (a
+    hipStream_t handle; default: torch's current stream)."""
+    import ctypes as C
+    import torch
+    from . import _native
+    from ._abi import PT_FLAG_OUT_F64
+    if gathered.dtype != out.dtype or gathered.dtype not in (torch.float32, torch.float64):
+        raise ValueError("gathered and out must both be float32 or both float64")
+    if not (gathered.is_contiguous() and out.is_contiguous()):
+        raise ValueError("gathered and out must be contiguous")
+    world, max_rows, W = gathered.shape[0], gathered.shape[1], gathered.shape[2]
+    H = out.shape[0]
+    if out.shape[1:] != (W, 3) or gathered.shape[3] != 3:
+        raise ValueError("shapes must be (world, max_rows, W, 3) and (H, W, 3)")
+    if stream is None:
+        stream = torch.cuda.current_stream().cuda_stream
+    flags = PT_FLAG_OUT_F64 if gathered.dtype == torch.float64 else 0
+    _native.check(_native.lib().pt_assemble_bands_device(
+        C.c_void_p(gathered.data_ptr()), world, max_rows, W, H, flags, C.c_void_p(out.data_ptr()),
+        C.c_void_p(stream)), "pt_assemble_bands_device")
+    return out
+
+
 def render_distributed(renderer, width, height, spp=1, bounces=1, seed=None, rr=False,
                        rr_depth=3, group=None, return_tiles=False):
     """Render `height` rows interleaved over the ranks of `group` on each

@@ -46,12 +46,13 @@ def render_ranks(scene, args, W, H):
     or None, f64 framebuffer) on rank 0, (None, None) elsewhere."""
     import torch
     import torch.distributed as dist
-    from .distributed import assemble, deinterleave, gather_tiles, max_band_rows
-    from .launch import rank_env
-    from .render import Renderer, image_u8, image_u8_device
+    from .distributed import assemble_bands_device, gather_tiles, max_band_rows
+    from .launch import pg_timeout, rank_env
+    from .render import Renderer, image_u8_device
     rank, local, world = rank_env()
     torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout())
+    ok = False
     try:
         with Renderer(scene) as r:
             p = r.params(W, H, args.n_rays, args.n_bounces, args.seed, args.rr, out_f64=True,
@@ -64,21 +65,24 @@ def render_ranks(scene, args, W, H):
                 print(f'render: {W}x{H}, {args.n_rays} spp, {args.n_bounces} bounces on {world} '
                       f'GPUs, rank-0 kernel {r.last_kernel_ms():.3f} ms')
         if rank != 0:
+            ok = True
             return None, None
-        if H % world == 0:
-            frame = deinterleave(torch.stack(tiles), torch.empty((H, W, 3), dtype=torch.float64,
-                                                                 device="cuda"))
-            arr = None
-            if W == H:
-                img = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
-                image_u8_device(frame.data_ptr(), W, H, True, img.data_ptr(),
-                                torch.cuda.current_stream().cuda_stream)
-                arr = img.cpu().numpy()
-            return arr, frame.cpu().numpy()
-        fb = assemble([t.cpu().numpy() for t in tiles], H)
-        return (image_u8(fb) if W == H else None), fb
+        frame = assemble_bands_device(torch.stack(tiles),
+                                      torch.empty((H, W, 3), dtype=torch.float64, device="cuda"))
+        arr = None
+        if W == H:
+            img = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+            image_u8_device(frame.data_ptr(), W, H, True, img.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+            arr = img.cpu().numpy()
+        ok = True
+        return arr, frame.cpu().numpy()
     finally:
-        dist.barrier()
+        # the closing barrier only on success: after an error here the peers
+        # may be blocked in the gather and would never reach it (the parent,
+        # launch.spawn_ranks, stops them once this rank exits non-zero)
+        if ok:
+            dist.barrier()
         dist.destroy_process_group()
 
 

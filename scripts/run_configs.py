@@ -72,7 +72,11 @@ with Renderer(scene_reader.Scene(CORNELL)) as r:
         rows = [300, 700]
         pix = [ix * H + iy for iy in rows for ix in range(0, W, 8)]
         linf, sec = check_pixels(r, fb, W, H, 1024, 8, pix, rr=True)
-        emit("K3", W, H, 1024, 8, True, ms, linf, len(pix), {"oracle_s": round(sec, 1)})
+        emit("K3", W, H, 1024, 8, True, ms, linf, len(pix),
+             {"oracle_s": round(sec, 1),
+              "parity": "RR leg parity unpinned: Russian roulette is a build extension (the "
+                        "reference ends paths only at -b, main.py:192-268); checked against the "
+                        "oracle's restatement of this build's RR rule"})
     if "K4" in only:
         # one GPU's share of K4 (4096^2, 4096 spp, 4 bounces over 8 GPUs): the
         # rows iy % 8 == 0, as rank 0 of bench.py's 8-GPU row interleave

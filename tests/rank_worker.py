@@ -4,7 +4,9 @@ their GPU ranks.  Renders this rank's interleaved row band with the CPU
 oracle (standing in for the HIP tile, which needs a GPU), gathers the tiles to
 rank 0 with distributed.gather_tiles and assembles the frame with
 distributed.deinterleave (the device-side assembly bench.py and the CLI use);
-rank 0 saves it to argv[1]."""
+rank 0 saves it to argv[1].  With PT_TEST_FAIL_RANK=r, rank r raises right
+after the rendezvous (the others go on into the gather and block there): the
+fail-fast test of launch.spawn_ranks."""
 import os
 import sys
 
@@ -19,15 +21,17 @@ from oracle import oracle  # noqa: E402
 from pathtracerpython_amd import scene_reader  # noqa: E402
 from pathtracerpython_amd.distributed import (band_rows_of, deinterleave, gather_tiles,  # noqa: E402
                                               max_band_rows)
-from pathtracerpython_amd.launch import rank_env  # noqa: E402
+from pathtracerpython_amd.launch import pg_timeout, rank_env  # noqa: E402
 from pathtracerpython_amd.pack import pack_scene  # noqa: E402
 
 
 def main():
     out, W, H, spp, B, seed = sys.argv[1], *map(int, sys.argv[2:7])
     rank, local, world = rank_env()
-    dist.init_process_group("gloo")
+    dist.init_process_group("gloo", timeout=pg_timeout())
     assert dist.get_rank() == rank and dist.get_world_size() == world
+    if os.environ.get("PT_TEST_FAIL_RANK") == str(rank):
+        raise RuntimeError(f"rank {rank}: injected failure after the rendezvous")
     scene_reader.VERBOSE = False
     pk = pack_scene(scene_reader.Scene(os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl")))
     rows = band_rows_of(H, rank, world)

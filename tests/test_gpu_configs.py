@@ -95,9 +95,9 @@ def test_k4_band_full(R, packed):
 
 
 def test_bands_assemble_when_lane_cap_binds(R):
-    """Lanes per pixel depend on the full image and spp, never on the band:
-    at 1024^2 x 512 spp (64 lanes per pixel, the cap) two interleaved bands
-    assemble to the 1-GPU frame bit for bit."""
+    """At 1024^2 x 512 spp every launch runs the lane cap (64 lanes per
+    pixel), the full frame and each band of a 2-way interleave alike, so the
+    bands assemble to the 1-GPU frame bit for bit."""
     from pathtracerpython_amd.distributed import assemble, max_band_rows
     W = H = 1024
     full = render_dev(R, R.params(W, H, 512, 1, 9, out_f64=True))

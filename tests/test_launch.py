@@ -28,6 +28,36 @@ def test_spawn_reports_failure():
     assert spawn_ranks(2, ["-c", "import os, sys; sys.exit(3 if os.environ['RANK'] == '1' else 0)"]) == 3
 
 
+def test_spawn_fails_fast_when_a_rank_dies_after_rendezvous(tmp_path, monkeypatch):
+    """Rank 1 raises after init_process_group while rank 0 goes on into the
+    gather: the parent must see rank 1's status and stop rank 0 within
+    seconds, not at the process group's timeout (reference: worker errors
+    re-raised at .get(), main.py:204)."""
+    import time
+    from pathtracerpython_amd.launch import spawn_ranks
+    monkeypatch.setenv("PT_TEST_FAIL_RANK", "1")
+    monkeypatch.setenv("PT_PG_TIMEOUT_S", "600")   # a blocked gather would wait this long
+    t0 = time.monotonic()
+    rc = spawn_ranks(2, [os.path.join(ROOT, "tests", "rank_worker.py"), str(tmp_path / "f.npy"),
+                         "10", "12", "2", "3", "9"])
+    dt = time.monotonic() - t0
+    assert rc != 0
+    assert dt < 60, dt
+    assert not (tmp_path / "f.npy").exists()
+
+
+def test_spawn_stops_siblings_of_a_failed_rank():
+    """A rank that never exits on its own (blocked) is terminated once a
+    sibling fails."""
+    import time
+    from pathtracerpython_amd.launch import spawn_ranks
+    t0 = time.monotonic()
+    rc = spawn_ranks(2, ["-c", "import os, sys, time\n"
+                               "if os.environ['RANK'] == '1': sys.exit(5)\n"
+                               "time.sleep(600)"])
+    assert rc == 5 and time.monotonic() - t0 < 30
+
+
 def test_deinterleave_matches_assemble():
     import torch
     from pathtracerpython_amd.distributed import assemble, deinterleave
