@@ -31,11 +31,12 @@ Printed on rank 0: one JSON line with the driver's fields plus
   roofline     : the dominant kernel's achieved rate against its roof.
                  k2/k4: k_render, FP32 VALU: reference-semantics ray-triangle
                  tests (exact, from a counting launch) x 47 FLOP (SURVEY.md
-                 §8d) / HIP-event kernel time, vs 157.3 TF/s.  k5: the shadow
-                 walk kernel, HBM: algorithmic bytes (node + leaf records +
-                 query records, from a counting launch) / its HIP-event time,
-                 vs 8 TB/s.  traffic: rocprofv3 PMC bytes per launch from
-                 profiles/, only when measured on the current kernel sources.
+                 §8d) / HIP-event kernel time, vs 157.3 TF/s.  k5: the BVH
+                 walk kernels (shadow and closest), L2 roof: algorithmic
+                 bytes (node + leaf records + query records, from a counting
+                 launch) / their HIP-event time.  traffic: rocprofv3 PMC
+                 bytes per launch from profiles/, only when measured on the
+                 current kernel sources (tests/test_profiles.py).
   cpu_baseline : the C oracle (f64 restatement of the reference loop, test
                  infrastructure) on this host's CPU share, on a bounded sample
   linf_vs_cpu_ref : per-pixel L-inf of this run's f32 framebuffer (as timed)
@@ -78,6 +79,10 @@ CONFIGS = {
 # record read (origin, group, direction, range bracket, key2/leak: 44 B), the
 # list entry (4 B) and its result written (<= 8 B)
 QNODE_B, UNITC_B, SHADOWQ_B, SHADOW_RES_B = 64, 64, 48, 8
+# closest walks: per query the whole WfClosestQ record read (48 B: origin,
+# group, direction, the uniform units' candidates), the list entry (4 B) and
+# the result written (a1, a2, b1, i1: 16 B)
+CLOSESTQ_B, CLOSEST_RES_B = 52, 16
 
 
 def parse():
@@ -108,6 +113,17 @@ def source_sha():
             h.update(open(os.path.join(csrc, f), "rb").read())
     h.update(open(os.path.join(ROOT, "include", "pt_capi.h"), "rb").read())
     return h.hexdigest()[:16]
+
+
+def load_traffic_record(config):
+    """profiles/traffic_<config>.json when measured on the current kernel
+    sources, else None."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{config}.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    return d if d.get("source_sha") == source_sha() else None
 
 
 def load_traffic(config):
@@ -322,12 +338,15 @@ def k_render_roofline(r, p, k_ms, W, rows, SPP, config):
 
 
 def k5_roofline(r, p, render_ms):
-    """The wavefront render's dominant kernel (the shadow walks, k_wf_shadow):
-    algorithmic bytes of its launches (counting launch) over their HIP-event
-    time (a profiling launch of the production kernels), against the L2 roof —
-    the BVH (7.5 MB) is served from the XCDs' L2 (91% hit) and the rate of its
-    record reads exceeds HBM's peak; the PMC traffic beyond L2 is reported
-    beside it as hbm_frac."""
+    """The wavefront render's two walk kernels (k_wf_shadow, k_wf_closest):
+    algorithmic bytes of their launches (counting launch) over their
+    HIP-event time (a profiling launch of the production kernels), against
+    the L2 roof — the BVH (9.6 MB of nodes and leaf records) is served from
+    the XCDs' L2 (~92% hit) and the rate of its record reads exceeds HBM's
+    peak; the PMC traffic beyond L2 is reported beside it as hbm_frac.  The
+    top-level object is the walk with the larger HIP-event time per render
+    (the two overlap on two streams: a walk's time includes the stretches it
+    waits for CUs the other one holds), the other one is `other_walk`."""
     from pathtracerpython_amd._abi import PT_FLAG_KERNEL_TIMES, PT_FLAG_WALK_COUNT, make_params
 
     def with_flags(f):
@@ -335,37 +354,47 @@ def k5_roofline(r, p, render_ms):
                            p.row_begin, p.row_end, p.row_step, p.row_phase, p.sample_begin)
     _, wc = r.render_params(with_flags(PT_FLAG_WALK_COUNT), stats=True)
     _, kt = r.render_params(with_flags(PT_FLAG_KERNEL_TIMES), stats=True)
-    nl = max(1, kt["shadow_launches"])
-    sh_bytes = (wc["shadow_node_visits"] * QNODE_B + wc["shadow_leaf_units"] * UNITC_B +
-                wc["shadow_queries"] * (SHADOWQ_B + SHADOW_RES_B))
-    per_launch = sh_bytes / nl
-    launch_ms = kt["shadow_ms"] / nl
-    achieved = per_launch / (launch_ms * 1e-3) / 1e9
-    traffic, tsrc = load_traffic("k5")
-    return {"bound": "l2", "achieved": round(achieved, 2), "peak": L2_GATHER_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / L2_GATHER_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "k_wf_shadow<true,false> (persistent one-ray shadow walks)",
-            "note": "latency-bound pointer chasing over an L2-resident BVH: the peak is the "
-                    "L2-served gather rate of MI355X_MICROARCH.md (16.8-18.8 TB/s); the record "
-                    "reads run above HBM's 8 TB/s, the PMC bytes beyond L2 are traffic / hbm_frac",
-            "hbm_frac": (round(traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                         if traffic else None),
-            "work_per_launch": {"shadow_rays": wc["shadow_queries"] / nl,
-                                "node_visits": wc["shadow_node_visits"] / nl,
-                                "leaf_unit_tests": wc["shadow_leaf_units"] / nl,
-                                "bytes": per_launch,
-                                "bytes_model": f"{QNODE_B} B per 4-wide node visit + {UNITC_B} B "
-                                               f"per leaf unit + {SHADOWQ_B}+{SHADOW_RES_B} B "
-                                               f"per shadow ray"},
-            "kernel_ms_mean": round(launch_ms, 4), "launches_per_render": nl,
-            "render_ms_mean": round(render_ms, 3),
-            "kernel_ms_per_render": {"shade": round(kt["shade_ms"], 2),
-                                     "shadow": round(kt["shadow_ms"], 2),
-                                     "closest": round(kt["closest_ms"], 2)},
-            "closest_walk": {"queries": wc["closest_queries"],
-                             "node_visits": wc["closest_node_visits"],
-                             "leaf_unit_tests": wc["closest_leaf_units"]},
-            "traffic_source": tsrc, "kernel_source_sha": source_sha()}
+    traffic = load_traffic_record("k5")
+
+    def walk(kind):
+        nl = max(1, kt[f"{kind}_launches"])
+        q_b = SHADOWQ_B + SHADOW_RES_B if kind == "shadow" else CLOSESTQ_B + CLOSEST_RES_B
+        total = (wc[f"{kind}_node_visits"] * QNODE_B + wc[f"{kind}_leaf_units"] * UNITC_B +
+                 wc[f"{kind}_queries"] * q_b)
+        per_launch = total / nl
+        launch_ms = kt[f"{kind}_ms"] / nl
+        achieved = per_launch / (launch_ms * 1e-3) / 1e9
+        tr = None
+        if traffic:
+            tr = traffic.get("hbm_bytes_per_launch" if kind == "shadow" else "closest_hbm_bytes_per_launch")
+        return {"bound": "l2", "achieved": round(achieved, 2), "peak": L2_GATHER_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / L2_GATHER_PEAK_GBS, 4), "traffic": tr,
+                "kernel": f"k_wf_{kind}<true,false> (persistent " +
+                          ("one-ray shadow walks)" if kind == "shadow" else "closest-hit walks)"),
+                "hbm_frac": (round(tr / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None),
+                "work_per_launch": {"queries": wc[f"{kind}_queries"] / nl,
+                                    "node_visits": wc[f"{kind}_node_visits"] / nl,
+                                    "leaf_unit_tests": wc[f"{kind}_leaf_units"] / nl,
+                                    "bytes": per_launch,
+                                    "bytes_model": f"{QNODE_B} B per 4-wide node visit + {UNITC_B} B "
+                                                   f"per leaf unit + {q_b} B per query (its record "
+                                                   f"read, list entry, result written)"},
+                "kernel_ms_mean": round(launch_ms, 4), "launches_per_render": nl,
+                "kernel_ms_per_render": round(kt[f"{kind}_ms"], 2)}
+    sh, cl = walk("shadow"), walk("closest")
+    top, other = (sh, cl) if kt["shadow_ms"] >= kt["closest_ms"] else (cl, sh)
+    top = dict(top)
+    top.update({"note": "latency-bound pointer chasing over an L2-resident BVH: the peak is the "
+                        "L2-served gather rate of MI355X_MICROARCH.md (16.8-18.8 TB/s); the record "
+                        "reads run above HBM's 8 TB/s, the PMC bytes beyond L2 are traffic / hbm_frac",
+                "other_walk": other,
+                "render_ms_mean": round(render_ms, 3),
+                "kernel_ms_per_render_all": {"shade": round(kt["shade_ms"], 2),
+                                             "shadow": round(kt["shadow_ms"], 2),
+                                             "closest": round(kt["closest_ms"], 2)},
+                "traffic_source": traffic.get("source") if traffic else
+                load_traffic("k5")[1], "kernel_source_sha": source_sha()})
+    return top
 
 
 def cpu_record(n_paths, seconds, threads, sample):
