@@ -130,6 +130,54 @@ __device__ __forceinline__ void store_pixel(const RenderK& R, const SlotJob& j, 
     }
 }
 
+// The primary ray's closest hit (main.py:191, :197-205), shared by the
+// `split` lanes of a pixel (scenes without a BVH): lane c tests the
+// eye-frame units c, c + split, ... (a per-lane unit index: vector loads of
+// the 128-B records), the group merges its candidate intervals with xor
+// shuffles, and every lane finishes the query as closest() does.  The merge
+// keeps closest_add's result except for the order among equal lower bounds,
+// and those never decide: closest_finish sends them to its f64 rescan (its
+// interval test b1 < a2 fails), so the hit is closest()'s bit for bit.  A
+// lane traces 1/split of the primary ray instead of all of it (K2 frame:
+// 32 lanes per pixel in one rank's band at N = 8, 64 in the tail rows).
+__device__ __forceinline__ ClosestAcc closest_merge(const ClosestAcc& x, const ClosestAcc& y) {
+    const bool yw = y.a1 < x.a1;   // (ties: x's, as closest_add keeps the first)
+    ClosestAcc r;
+    r.a1 = yw ? y.a1 : x.a1;
+    r.b1 = yw ? y.b1 : x.b1;
+    r.i1 = yw ? y.i1 : x.i1;
+    r.a2 = fminf(fminf(x.a2, y.a2), yw ? x.a1 : y.a1);
+    return r;
+}
+__device__ __forceinline__ int primary_shared(const SceneK& S, D3 eye, D3 d0, uint32_t c, uint32_t split,
+                                              const Spill& sp, D3* P0) {
+    const D3 dn = unit(d0);
+    sp.put3(kSpP, eye);
+    sp.put3(kSpNd, d0);
+    const F3 o32 = to_f3(eye - ld3(S.center));
+    const F3 d32 = to_f3(dn);
+    ClosestAcc acc = closest_init();
+    for (int u = (int)c; u < S.n_unit; u += (int)split) {
+        const UnitF U = S.unit_eye[u];
+        closest_unit<false>(S, U, origin_u(U, o32), d32, U.grp == -1, sp, kSpP, kSpNd, &acc, nullptr);
+    }
+    for (uint32_t m = 1; m < split; m <<= 1) {   // the pixel's lanes: one wave
+        ClosestAcc y;
+        y.a1 = __shfl_xor(acc.a1, (int)m);
+        y.a2 = __shfl_xor(acc.a2, (int)m);
+        y.b1 = __shfl_xor(acc.b1, (int)m);
+        y.i1 = __shfl_xor(acc.i1, (int)m);
+        acc = closest_merge(acc, y);
+    }
+    return closest_finish<false, false, false>(S, acc, eye, dn, P0, nullptr);
+}
+// from this many lanes per pixel on (wave-uniform): N = 8 band of the K2
+// frame (32 lanes) 0.765 -> 0.750 ms; at 8 lanes (N = 1) the vector loads
+// and the merge cost more than the 7/8 of the trace they save (+0.5%)
+#ifndef PT_PRIMARY_SHARED
+#define PT_PRIMARY_SHARED 16
+#endif
+
 template <bool FORCE64, bool COUNT, bool BVH>
 // 4 waves/SIMD (<= 128 VGPRs, a little scratch spill outside the triangle
 // loops): 9.5 ms vs 10.8 ms at 3 waves and 15.3 ms at 2 on the 512^2 x 64spp
@@ -172,7 +220,13 @@ __global__ __launch_bounds__(256, PT_RENDER_WAVES) void k_render(SceneK S, Rende
         J.rr_depth = R.rr_depth;
         D3 P0 = d3(0, 0, 0);
         int tri0 = -1;
-        if (ns > 0 && R.bounces > 0) tri0 = closest<FORCE64, false, BVH>(S, eye, d0, -1, sp, &P0, &cnt, true);
+        // (a pixel's lanes are all valid or all invalid, and split <= spp
+        // gives every lane samples: the whole group takes this branch)
+        if (PT_PRIMARY_SHARED && !FORCE64 && !BVH && split >= PT_PRIMARY_SHARED) {
+            if (R.bounces > 0) tri0 = primary_shared(S, eye, d0, c, split, sp, &P0);
+        } else if (ns > 0 && R.bounces > 0) {
+            tri0 = closest<FORCE64, false, BVH>(S, eye, d0, -1, sp, &P0, &cnt, true);
+        }
         acc = render_lane<FORCE64, COUNT, BVH>(S, J, d0, tri0, P0, sp, &cnt);
     }
     SlotJob j;

@@ -2,7 +2,8 @@
 (DESIGN.md §8).  For the built library (or PT_HIP_LIB): the kernel time of one
 rank's interleaved row band (row_step N, phases 0 and N-1) at N = 1/2/4/8,
 median of the last half of `launches`; then the fixed per-step legs on this
-GPU: the device de-interleave of the gathered tiles (bench.py's step) and,
+GPU: the device assembly of the gathered tiles (bench.py's step: the native
+pt_assemble_bands_device, and torch's strided copy for comparison) and,
 for reference, the PCIe D2H of the frame (outside bench.py's timed step).
 Prints one JSON object per line.
 Usage: prof_scaling.py [launches] [N...]"""
@@ -54,11 +55,14 @@ def ev_time(fn, reps=50):
 
 
 if lib == "libpt_hip.so":
+    from pathtracerpython_amd.distributed import assemble_bands_device
     for N in (2, 4, 8):
         g = torch.rand((N, H // N, W, 3), device="cuda")
         f = torch.empty((H, W, 3), device="cuda")
-        print(json.dumps({"leg": "deinterleave", "N": N,
+        print(json.dumps({"leg": "deinterleave_torch", "N": N,
                           "ms": round(ev_time(lambda: deinterleave(g, f)), 4)}), flush=True)
+        print(json.dumps({"leg": "assemble_bands_device", "N": N,
+                          "ms": round(ev_time(lambda: assemble_bands_device(g, f)), 4)}), flush=True)
     host = torch.empty((H, W, 3), dtype=torch.float32).pin_memory()
     print(json.dumps({"leg": "d2h_pinned_3MB", "ms": round(ev_time(lambda: host.copy_(tile, non_blocking=True)), 4)}),
           flush=True)
