@@ -40,6 +40,10 @@ pmc k2_sq2 "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCL
 pmc k2_sq3 "GRBM_GUI_ACTIVE GRBM_COUNT SQ_THREAD_CYCLES_VALU SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS SQ_INSTS_VALU_TRANS_F32" "$R/scripts/prof_k2.py" 2
 python3 "$R/scripts/summarize_pmc.py" "$P/${TAG}_pmc_k2_sq.json" "$OUT/k2_sq1" "$OUT/k2_sq2" "$OUT/k2_sq3" > /dev/null
 cd "$R"
+# the box's copy of the repo reads the new stamp, so this run's bench lines
+# carry the traffic just measured (profiles/ here is a scratch copy: the
+# staged files are installed by install_profiles.py)
+cp "$P/traffic_k2.json" "$R/profiles/traffic_k2.json"
 # 3-4. K2 bench: rocprof stats of the bench command, then the line itself
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_k2" -o k2 \
     -- python3 "$R/bench.py" --steps 50 --no-cpu-baseline --no-check > "$OUT/trace_k2.log" 2>&1
@@ -62,5 +66,6 @@ python3 "$R/scripts/stamp_traffic.py" "$P/${TAG}_pmc_k5_traffic.json" "$P/traffi
     "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), k_wf_shadow, 1024x1024 256spp 4b, mean over its dispatches; profiles/${TAG}_pmc_k5_traffic.json; FETCH doubled (gfx950)" \
     "$P/${TAG}_pmc_k5_closest_traffic.json"
 cd "$R"
+cp "$P/traffic_k5.json" "$R/profiles/traffic_k5.json"
 timeout -k 10 400 python3 "$R/bench.py" --config k5 > "$P/${TAG}_bench_k5.json" 2> "$OUT/bench_k5.err"
 cat "$P/${TAG}_bench_k5.json"
