@@ -189,6 +189,7 @@ __global__ __launch_bounds__(256, PT_RENDER_WAVES) void k_render(SceneK S, Rende
                                                 StatsDev* __restrict__ st) {
     __shared__ double spill[kSpillSlots][256];
     const Spill sp{&spill[0][threadIdx.x], 256};
+    PT_STAMP(k0);
     // (slot_job's mapping written out: the register allocation of this kernel
     // is sensitive to what stays live across the render loop)
     const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
@@ -227,8 +228,20 @@ __global__ __launch_bounds__(256, PT_RENDER_WAVES) void k_render(SceneK S, Rende
         } else if (ns > 0 && R.bounces > 0) {
             tri0 = closest<FORCE64, false, BVH>(S, eye, d0, -1, sp, &P0, &cnt, true);
         }
+#if defined(PT_PHASE_CLOCKS)
+        {
+            PT_STAMP(k1);
+            PT_PHASE_FLUSH_AT(5, k1 - k0);
+        }
+#endif
         acc = render_lane<FORCE64, COUNT, BVH>(S, J, d0, tri0, P0, sp, &cnt);
     }
+#if defined(PT_PHASE_CLOCKS)
+    {
+        PT_STAMP(k2);
+        PT_PHASE_FLUSH_AT(6, k2 - k0);
+    }
+#endif
     SlotJob j;
     j.valid = valid;
     j.c = c;
@@ -735,6 +748,19 @@ static int dev_alloc_copy(T** d, const T* h, size_t n) {
     if (h) HIPCHK(hipMemcpy(*d, h, n * sizeof(T), hipMemcpyHostToDevice));
     return PT_OK;
 }
+
+#if defined(PT_PHASE_CLOCKS)
+// dev builds only (scripts/phase_clocks.py): the phase clocks of pt_path.h
+extern "C" int pt_debug_phase_clocks(unsigned long long* out, int reset) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(pt_phase_clk), 8 * sizeof(unsigned long long)));
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pt_phase_clk), z, sizeof(z)));
+    }
+    return PT_OK;
+}
+#endif
 
 extern "C" {
 

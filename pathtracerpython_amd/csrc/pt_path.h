@@ -1412,6 +1412,44 @@ struct LaneJob {
     int32_t rr_depth;        // < 0: no Russian roulette
 };
 
+// Phase clocks (dev builds only, -DPT_PHASE_CLOCKS; scripts/phase_clocks.py):
+// shader-clock cycles (s_memtime) a wave spends in each part of the bounce
+// loop, summed over waves into pt_phase_clk[]: 0 RNG + light samples + next
+// ray, 1 the uniform units' fused pass, 2 the BVH and the light's units,
+// 3 the colour, the next hit and path regeneration, 4 loop iterations,
+// 5 the primary ray, 6 the whole lane (k_render)
+#if defined(PT_PHASE_CLOCKS) && defined(__HIP__)
+__device__ unsigned long long pt_phase_clk[8];   // (both passes: the host reads it)
+#endif
+#if defined(PT_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+#define PT_STAMP(t) const uint64_t t = (uint64_t)__builtin_amdgcn_s_memtime()
+#define PT_PHASE(i, v) ph[i] += (v)
+// one value v into pt_phase_clk[i]: the maximum over the wave's ACTIVE
+// lanes (an inactive partner of the xor butterfly counts as 0: its
+// registers are not this value), added once per wave
+__device__ inline void pt_phase_flush_at(int i, uint64_t v) {
+    const uint64_t act = __ballot(1);
+    const int lane = (int)__lane_id();
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint64_t o = (uint64_t)__shfl_xor((unsigned long long)v, m);
+        if (!((act >> (lane ^ m)) & 1ull)) o = 0;
+        v = o > v ? o : v;
+    }
+    if (lane == __ffsll((unsigned long long)act) - 1) atomicAdd(&pt_phase_clk[i], (unsigned long long)v);
+}
+// a wave's time in a phase is its last lane's (active in every iteration)
+#define PT_PHASE_FLUSH(n)                                     \
+    do {                                                      \
+        for (int i_ = 0; i_ < (n); ++i_) pt_phase_flush_at(i_, ph[i_]); \
+    } while (0)
+#define PT_PHASE_FLUSH_AT(i, v) pt_phase_flush_at((i), (v))
+#else
+#define PT_STAMP(t)
+#define PT_PHASE(i, v)
+#define PT_PHASE_FLUSH(n)
+#define PT_PHASE_FLUSH_AT(i, v)
+#endif
+
 // All samples of one lane for one pixel; returns the SUM of sample colours.
 // Paths are regenerated in place: when a path ends the lane starts its next
 // sample from the cached primary hit (primary rays are identical for every
@@ -1449,7 +1487,11 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
         bump<COUNT>(cnt, &Counters::ray_bounces, 1);
     }
+#if defined(PT_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+    uint64_t ph[5] = {0, 0, 0, 0, 0};
+#endif
     while (active) {
+        PT_STAMP(c0);
         const D3 P = sp.get3(kSpP);   // this bounce's origin
         const uint32_t sample = (uint32_t)(J.sample0 + si * J.sample_stride);
         const int obj = S.tri_obj[tri];
@@ -1502,6 +1544,8 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
         const F3 n32 = to_f3(unit(nd));
         ClosestAcc ca = closest_init();
         const bool any_trace = PT_WAVE_ANY(trace);
+        PT_STAMP(c1);
+        PT_PHASE(0, c1 - c0);
         if (!FORCE64 && !COUNT && PT_MARGIN) {   // occlusion as margins (> 0: occluded)
             float oc[kLightSamples] = {-1.0f, -1.0f, -1.0f};
             for (int u = 0; u < S.n_obj_unit; ++u) {
@@ -1527,6 +1571,8 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
                                            &ca, sp, cnt);
             }
         }
+        PT_STAMP(c2);
+        PT_PHASE(1, c2 - c1);
         if (BVH && S.n_bnode) {   // the meshes: shadows as a packet, the closest ray ordered
             const F3 o32 = to_f3(P - ld3(S.center));   // the BVH's frame
             const bool ordered = !FORCE64 && S.bvh_depth < kBvhStack;
@@ -1547,6 +1593,8 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
                                     &ca, cnt);
             }
         }
+        PT_STAMP(c3);
+        PT_PHASE(2, c3 - c2);
         {   // l_k . n again from the homes, with shadow_setup's operations:
             // recomputed rather than carried across the unit loops (-0.05 ms)
             const D3 Pc = sp.get3(kSpP), nc = ld3(S.tris[tri].n);
@@ -1592,7 +1640,11 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
                 }
             }
         }
+        PT_STAMP(c4);
+        PT_PHASE(3, c4 - c3);
+        PT_PHASE(4, 1);
     }
+    PT_PHASE_FLUSH(5);
     return acc;
 }
 

@@ -4,6 +4,8 @@
 #   2. the band-scaling sweep (scripts/prof_scaling.py) -> scaling.jsonl
 #   3. the profile refresh (scripts/refresh_profiles.sh TAG), staged for
 #      scripts/install_profiles.py
+#   4. every single-GPU BASELINE config at full size (scripts/run_configs.py)
+#      -> staged as profiles/TAG_configs.jsonl
 # Usage: gpurun -- bash scripts/gpu_round.sh TAG
 # Each GPU step has its own time limit; a failed test run stops before the
 # measurements, a fault or timeout stops everything.
@@ -21,4 +23,6 @@ cat "$OUT/scaling.jsonl"
 bash scripts/refresh_profiles.sh "$TAG" > "$OUT/refresh.log" 2>&1
 rc=$?
 tail -4 "$OUT/refresh.log"
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python3 -u scripts/run_configs.py 2>&1 | grep -v amdgpu.ids \
+    | tee "gpurun_out/refresh_$TAG/profiles/${TAG}_configs.jsonl"

@@ -3,9 +3,9 @@ MI355X and record kernel time, throughput and parity checks (dev tool; the
 bench line is bench.py's K2).  Writes one JSON object per line to stdout.
 
   K1  64x64, 1 spp, 1 bounce        whole image vs the CPU oracle, hybrid == forced-f64
-  K2  512x512, 64 spp, 4 bounces    = bench.py's workload; oracle on 4 rows
+  K2  512x512, 64 spp, 4 bounces    = bench.py's workload; oracle on every pixel
   K3  1024x1024, 1024 spp, 8 b + RR oracle on 2 rows (all 1024 spp)
-  K5  100k-triangle mesh, 1024x1024, 256 spp, 4 b   oracle on 64 pixels
+  K5  100k-triangle mesh, 1024x1024, 256 spp, 4 b   oracle on 32 pixels
   K4  4096x4096, 4096 spp, 4 b: one GPU's row band (iy % 8 == 0) of the 8-GPU split;
       oracle on 32 pixels of the band
 Usage: run_configs.py [K1,K2,K3,K4,K5]"""
@@ -63,9 +63,8 @@ with Renderer(scene_reader.Scene(CORNELL)) as r:
     if "K2" in only:
         W = H = 512
         fb, ms = timed(r, W, H, 64, 4)
-        rows = [0, 131, 262, 511]
-        linf, _ = check_pixels(r, fb, W, H, 64, 4, [ix * H + iy for iy in rows for ix in range(W)])
-        emit("K2", W, H, 64, 4, False, ms, linf, 4 * W)
+        linf, _ = check_pixels(r, fb, W, H, 64, 4, range(W * H))   # the whole frame
+        emit("K2", W, H, 64, 4, False, ms, linf, W * H)
     if "K3" in only:
         W = H = 1024
         fb, ms = timed(r, W, H, 1024, 8, rr=True, reps=1)
@@ -106,7 +105,7 @@ if "K5" in only:
         W = H = 1024
         fb, ms = timed(r, W, H, 256, 4, reps=1)
         rs = np.random.RandomState(0)
-        pix = sorted(rs.choice(W * H, 64, replace=False).tolist())
+        pix = sorted(rs.choice(W * H, 32, replace=False).tolist())
         linf, sec = check_pixels(r, fb, W, H, 256, 4, pix)
         small = r.render(64, 64, 2, 4, 9, out_f64=True)
         small64 = r.render(64, 64, 2, 4, 9, out_f64=True, force_f64=True)

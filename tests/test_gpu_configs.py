@@ -3,7 +3,7 @@ C-ABI, against the CPU oracle on pixel subsets plus size-independent
 properties over the whole launch.  Each config is the reference loop
 /root/reference/main.py:186-280 at that size.
 
-Pixel subsets cover the bottom, middle and top rows of each image (the top
+Pixel subsets cover whole bottom, middle and top rows of each image (the top
 sixteenth of rows is dispatched last and, at K2-like spp, runs at 8x lanes per
 pixel).  Tolerance: f64 framebuffer, L-inf <= 1e-12 (the
 kernel's path state is f64 and every hit/miss decision is exact; BASELINE.json's
@@ -60,15 +60,18 @@ def check_oracle(packed, fb_row_of, W, H, spp, B, picks, flags=0):
 
 def test_k3_full(R, packed):
     """K3: Cornell 1024x1024, 1024 spp, 8 bounces + Russian roulette (one
-    ~0.5-s launch).  Oracle on 96 pixels over bottom, middle and top (tail)
-    rows; finite everywhere; the same rows rendered as a band of two sample
-    halves (sample_begin) average to the full render."""
+    ~0.5-s launch).  Oracle on 4 whole rows (4,096 pixels: the bottom, two
+    middle rows and the top row, in the tail dispatched last) plus 32 pixels
+    spread over 2 more rows; finite everywhere; the same rows rendered as a
+    band of two sample halves (sample_begin) average to the full render.
+    (The RR leg is parity unpinned: the reference has no roulette.)"""
     from pathtracerpython_amd._abi import PT_FLAG_RR
     W = H = 1024
     p = R.params(W, H, 1024, 8, 9, rr=True, out_f64=True)
     fb = render_dev(R, p)
     assert np.isfinite(fb).all()
-    picks = spread_pixels(W, [0, 1, 511, 512, 980, 1023], 16, 3)
+    picks = [(ix, iy) for iy in (0, 511, 512, 1023) for ix in range(W)]
+    picks += spread_pixels(W, [1, 980], 16, 3)
     check_oracle(packed, lambda iy: fb[H - 1 - iy], W, H, 1024, 8, picks, flags=PT_FLAG_RR)
     # sample-split property on an interleaved band (rows iy % 64 == 5)
     band = dict(row_step=64, row_phase=5)
@@ -81,8 +84,9 @@ def test_k3_full(R, packed):
 
 def test_k4_band_full(R, packed):
     """K4: Cornell 4096x4096, 4096 spp, 4 bounces over 8 GPUs — one GPU's
-    interleaved row band (iy % 8 == 3, 512 rows, ~3 s): oracle on 32 pixels
-    over its bottom, middle and top rows; finite everywhere."""
+    interleaved row band (iy % 8 == 3, 512 rows, ~3 s): oracle on the band's
+    bottom and top rows in full (2 x 4,096 pixels x 4,096 spp) and 32 pixels
+    over three more rows; finite everywhere."""
     W = H = 4096
     p = R.params(W, H, 4096, 4, 9, out_f64=True, row_step=8, row_phase=3)
     fb = render_dev(R, p)
@@ -90,7 +94,8 @@ def test_k4_band_full(R, packed):
     assert np.isfinite(fb).all()
     rows = list(range(3, H, 8))[::-1]          # framebuffer order, top first
     pos = {iy: j for j, iy in enumerate(rows)}
-    picks = spread_pixels(W, [3, 11, 2051, 3843, 4091], 6, 4) + [(0, 3), (W - 1, 4091)]
+    picks = [(ix, iy) for iy in (3, 4091) for ix in range(W)]
+    picks += spread_pixels(W, [11, 2051, 3843], 10, 4) + [(0, 2051), (W - 1, 3843)]
     check_oracle(packed, lambda iy: fb[pos[iy]], W, H, 4096, 4, picks)
 
 
