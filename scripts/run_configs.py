@@ -25,9 +25,16 @@ only = sys.argv[1].split(",") if len(sys.argv) > 1 else ["K1", "K2", "K3", "K4",
 
 
 def timed(r, W, H, spp, B, rr=False, reps=2, **band):
+    """min kernel ms of `reps` launches after 10 ms of warm-up launches (a
+    fresh box ramps its clock over the first launches: 7.3 -> 5.6 ms at K2)"""
     p = r.params(W, H, spp, B, 9, rr=rr, out_f64=True, **band)
     fb = torch.zeros((r.band_rows(p), W, 3), dtype=torch.float64, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
+    warm = 0.0
+    while warm < 50.0:   # at least ~50 ms of the same launch first
+        r.render_device(p, fb.data_ptr(), s)
+        torch.cuda.synchronize()
+        warm += r.last_kernel_ms()
     ms = []
     for _ in range(reps):
         r.render_device(p, fb.data_ptr(), s)
