@@ -1437,10 +1437,24 @@ __device__ inline void pt_phase_flush_at(int i, uint64_t v) {
     }
     if (lane == __ffsll((unsigned long long)act) - 1) atomicAdd(&pt_phase_clk[i], (unsigned long long)v);
 }
-// a wave's time in a phase is its last lane's (active in every iteration)
+// the sum over the wave's active lanes into pt_phase_clk[i]
+__device__ inline void pt_phase_flush_sum(int i, uint64_t v) {
+    const uint64_t act = __ballot(1);
+    const int lane = (int)__lane_id();
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint64_t o = (uint64_t)__shfl_xor((unsigned long long)v, m);
+        if (!((act >> (lane ^ m)) & 1ull)) o = 0;
+        v += o;
+    }
+    if (lane == __ffsll((unsigned long long)act) - 1) atomicAdd(&pt_phase_clk[i], (unsigned long long)v);
+}
+// a wave's time in a phase is its last lane's (active in every iteration);
+// slot 7: the lanes' own iteration counts summed (tail utilisation = slot 7
+// / (64 x slot 4) for full waves)
 #define PT_PHASE_FLUSH(n)                                     \
     do {                                                      \
         for (int i_ = 0; i_ < (n); ++i_) pt_phase_flush_at(i_, ph[i_]); \
+        pt_phase_flush_sum(7, ph[4]);                         \
     } while (0)
 #define PT_PHASE_FLUSH_AT(i, v) pt_phase_flush_at((i), (v))
 #else

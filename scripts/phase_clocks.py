@@ -36,10 +36,14 @@ for _ in range(n):
     ms.append(r.last_kernel_ms())
 fn(clk, 1)
 names = ["setup_rng_lights_bounce", "uniform_unit_pass", "bvh_and_light_units", "colour_next_hit_regen",
-         "iterations", "primary_ray", "lane_total"]
+         "iterations", "primary_ray", "lane_total", "lane_iterations"]
 v = {k: clk[i] / n for i, k in enumerate(names)}
+names = names[:7]
 loop = sum(v[k] for k in names[:4])
 out = {"row_step": step, "kernel_ms": ms, "per_launch": v,
        "fraction_of_lane_total": {k: round(v[k] / v["lane_total"], 4) for k in names[:4] + ["primary_ray"]},
-       "fraction_of_bounce_loop": {k: round(v[k] / loop, 4) for k in names[:4]}}
+       "fraction_of_bounce_loop": {k: round(v[k] / loop, 4) for k in names[:4]},
+       # lanes active in the wave's bounce-loop iterations (the rest: lanes
+       # out of samples, waiting for the wave's longest lane)
+       "tail_lane_utilisation": round(v["lane_iterations"] / (64 * v["iterations"]), 4)}
 print(json.dumps(out), flush=True)
