@@ -1464,50 +1464,54 @@ __device__ inline void pt_phase_flush_sum(int i, uint64_t v) {
 #define PT_PHASE_FLUSH_AT(i, v)
 #endif
 
-// All samples of one lane for one pixel; returns the SUM of sample colours.
-// Paths are regenerated in place: when a path ends the lane starts its next
-// sample from the cached primary hit (primary rays are identical for every
-// sample, main.py:191), so a wave keeps tracing until all its lanes are out
-// of samples.
-template <bool FORCE64, bool COUNT, bool BVH = true>
-PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
-                     const Spill& sp, Counters* cnt) {
-    D3 acc = d3(0, 0, 0);
-    if (J.n_samples <= 0 || J.bounces <= 0) return acc;   // main.py:192 never runs
-    if (tri0 < 0 || tri0 >= S.n_obj_tri) {   // primary ray escapes or hits the light
-        const D3 v = tri0 < 0 ? d3(0, 0, 0) : ld3(S.light_rgb);
-        for (int i = 0; i < J.n_samples; ++i) {
-            acc = acc + v;
-            if (COUNT) {
-                bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
-                bump<COUNT>(cnt, &Counters::ray_bounces, 1);
-                bump<COUNT>(cnt, &Counters::escapes, tri0 < 0 ? 1u : 0u);
-                bump<COUNT>(cnt, &Counters::light_hits, tri0 < 0 ? 0u : 1u);
-            }
+// Sample scheduling of the bounce loop (render_loop): which sample a lane
+// traces next once its path ends.  LaneSched: the lane's own samples
+// sample0, sample0 + stride, ... (the host build, counting launches, BVH
+// scenes, the wavefront kernels' order); pt_hip.hip's WavePool: the samples
+// of a wave's pixels, handed out as lanes free up.
+struct LaneSched {
+    const LaneJob& J;
+    int tri0;
+    int si;
+    PT_HD uint32_t sample() const { return (uint32_t)(J.sample0 + si * J.sample_stride); }
+    PT_HD uint32_t pixel() const { return J.pixel; }
+    // after an iteration; `done`: this lane's path ended.  Starts the lane's
+    // next sample from the cached primary hit (primary rays are identical for
+    // every sample, main.py:191); false when it has none left.
+    template <bool COUNT>
+    PT_HD bool advance(const SceneK& S, bool done, const Spill& sp, int* tri, D3*, Counters* cnt) {
+        if (!done) return true;
+        if (++si >= J.n_samples) return false;
+        *tri = tri0;
+        sp.put3(kSpP, sp.get3(kSpP0));
+        sp.put3(kSpNd, d3(sp.get(kSpD0), sp.get(kSpD0 + 1), 0.0 - S.eye[2]));
+        if (COUNT) {
+            bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
+            bump<COUNT>(cnt, &Counters::ray_bounces, 1);
         }
-        return acc;
+        return true;
     }
-    int si = 0;
+};
+
+// The bounce loop: paths are regenerated in place (Sched::advance), so a
+// wave keeps tracing until all its lanes are out of samples.  The lane's
+// first path starts at tri, origin and direction in the homes kSpP / kSpNd;
+// sample colours are added to *acc.
+template <bool FORCE64, bool COUNT, bool BVH, class Sched>
+PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& sp, Counters* cnt,
+                       Sched& q, D3* accp) {
+    D3 acc = *accp;
     int b = 0;
-    int tri = tri0;
     double k = 1.0;
     bool active = true;
-    sp.put(kSpD0, d0.x);
-    sp.put(kSpD0 + 1, d0.y);
-    sp.put3(kSpP0, P0);
-    sp.put3(kSpP, P0);
-    sp.put3(kSpNd, d0);   // incoming direction of bounce 0 (main.py:191)
-    if (COUNT) {   // the cached primary trace, counted per sample
-        bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
-        bump<COUNT>(cnt, &Counters::ray_bounces, 1);
-    }
 #if defined(PT_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
     uint64_t ph[5] = {0, 0, 0, 0, 0};
 #endif
     while (active) {
         PT_STAMP(c0);
         const D3 P = sp.get3(kSpP);   // this bounce's origin
-        const uint32_t sample = (uint32_t)(J.sample0 + si * J.sample_stride);
+        const uint32_t sample = q.sample();
+        const uint32_t pixel = q.pixel();
         const int obj = S.tri_obj[tri];
         const TriS R = S.tris[tri];
         const Mat& m = S.mat[obj];
@@ -1522,16 +1526,16 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
 #pragma unroll
         for (int k = 0; k < kLightSamples; ++k) {
             uint32_t c[4];
-            rng_block(J.seed, J.pixel, sample, (uint32_t)b, (uint32_t)k, c);
+            rng_block(J.seed, pixel, sample, (uint32_t)b, (uint32_t)k, c);
             shadow_setup_k<COUNT>(S, P, ld3(R.n), k, u_of(c[0]), u_of(c[1]), u_of(c[2]), u_of(c[3]),
                                   &sh, sp);
         }
         sh.key2 = COUNT ? S.n_tri : S.n_obj;
         sh.leak = S.n_obj - 1;
-        rng_block(J.seed, J.pixel, sample, (uint32_t)b, 3u, &w[12]);
+        rng_block(J.seed, pixel, sample, (uint32_t)b, 3u, &w[12]);
 #else
         uint32_t w[16];
-        rng_blocks4(J.seed, J.pixel, sample, (uint32_t)b, w);
+        rng_blocks4(J.seed, pixel, sample, (uint32_t)b, w);
         {
             double u12[12];
 #pragma unroll
@@ -1638,27 +1642,50 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
                 ++b;
             }
         }
+        active = q.template advance<COUNT>(S, done, sp, &tri, &acc, cnt);
         if (done) {
-            ++si;
-            if (si >= J.n_samples) {
-                active = false;
-            } else {   // next sample from the cached primary hit
-                b = 0;
-                tri = tri0;
-                k = 1.0;
-                sp.put3(kSpP, sp.get3(kSpP0));
-                sp.put3(kSpNd, d3(sp.get(kSpD0), sp.get(kSpD0 + 1), 0.0 - S.eye[2]));
-                if (COUNT) {
-                    bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
-                    bump<COUNT>(cnt, &Counters::ray_bounces, 1);
-                }
-            }
+            b = 0;
+            k = 1.0;
         }
         PT_STAMP(c4);
         PT_PHASE(3, c4 - c3);
         PT_PHASE(4, 1);
     }
     PT_PHASE_FLUSH(5);
+    *accp = acc;
+}
+
+// All samples of one lane for one pixel (LaneSched); returns the SUM of
+// sample colours.
+template <bool FORCE64, bool COUNT, bool BVH = true>
+PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
+                     const Spill& sp, Counters* cnt) {
+    D3 acc = d3(0, 0, 0);
+    if (J.n_samples <= 0 || J.bounces <= 0) return acc;   // main.py:192 never runs
+    if (tri0 < 0 || tri0 >= S.n_obj_tri) {   // primary ray escapes or hits the light
+        const D3 v = tri0 < 0 ? d3(0, 0, 0) : ld3(S.light_rgb);
+        for (int i = 0; i < J.n_samples; ++i) {
+            acc = acc + v;
+            if (COUNT) {
+                bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
+                bump<COUNT>(cnt, &Counters::ray_bounces, 1);
+                bump<COUNT>(cnt, &Counters::escapes, tri0 < 0 ? 1u : 0u);
+                bump<COUNT>(cnt, &Counters::light_hits, tri0 < 0 ? 0u : 1u);
+            }
+        }
+        return acc;
+    }
+    sp.put(kSpD0, d0.x);
+    sp.put(kSpD0 + 1, d0.y);
+    sp.put3(kSpP0, P0);
+    sp.put3(kSpP, P0);
+    sp.put3(kSpNd, d0);   // incoming direction of bounce 0 (main.py:191)
+    if (COUNT) {   // the cached primary trace, counted per sample
+        bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
+        bump<COUNT>(cnt, &Counters::ray_bounces, 1);
+    }
+    LaneSched q{J, tri0, 0};
+    render_loop<FORCE64, COUNT, BVH>(S, J, tri0, sp, cnt, q, &acc);
     return acc;
 }
 
