@@ -1091,6 +1091,40 @@ PT_HD float q_child_dist(const QNode& Q, int c, const QLine& L, float R) {
     const float d = fmaxf(fmaxf(tmin, -tmax), 0.0f);
     return ((tmin <= tmax) & (d <= R)) ? d : INFINITY;
 }
+// The same distance with the node's code words ordered along the line:
+// near[a] holds the bounds the line meets first on axis a (qlo when A[a] > 0,
+// qhi when A[a] < 0; A is never zero, rcp_dir).  fma(q, A, B) is monotone in
+// q, so the near bound's t IS min(x0, x1) and the far bound's max(x0, x1):
+// bit for bit the same result without the per-child min / max pairs (one
+// word select per axis and node instead; hc_qbvh_check compares the two).
+struct QSlabs { uint32_t near[3], far[3]; };
+PT_HD QSlabs q_slabs(const QNode& Q, const QLine& L) {
+    QSlabs s;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const bool neg = L.A[a] < 0.0f;
+        s.near[a] = neg ? Q.qhi[a] : Q.qlo[a];
+        s.far[a] = neg ? Q.qlo[a] : Q.qhi[a];
+    }
+    return s;
+}
+PT_HD float q_child_dist_s(const QSlabs& s, int c, const QLine& L, float R) {
+    const float xn = fmaf(q_byte(s.near[0], c), L.A[0], L.B[0]), xf = fmaf(q_byte(s.far[0], c), L.A[0], L.B[0]);
+    const float yn = fmaf(q_byte(s.near[1], c), L.A[1], L.B[1]), yf = fmaf(q_byte(s.far[1], c), L.A[1], L.B[1]);
+    const float zn = fmaf(q_byte(s.near[2], c), L.A[2], L.B[2]), zf = fmaf(q_byte(s.far[2], c), L.A[2], L.B[2]);
+    const float tmin = fmaxf(fmaxf(xn, yn), zn);
+    const float tmax = fminf(fminf(xf, yf), zf);
+    const float d = fmaxf(fmaxf(tmin, -tmax), 0.0f);
+    return ((tmin <= tmax) & (d <= R)) ? d : INFINITY;
+}
+#ifndef PT_QSLABS
+#define PT_QSLABS 1
+#endif
+#if PT_QSLABS
+#define PT_QDIST(Q, S, c, L, R) q_child_dist_s((S), (c), (L), (R))
+#else
+#define PT_QDIST(Q, S, c, L, R) q_child_dist((Q), (c), (L), (R))
+#endif
 // 4 (distance, ref, rays) triples in ascending distance (sorting network)
 PT_HD void q_sort4(float d[4], int r[4], uint32_t m[4]) {
     auto cs = [&](int i, int j) {
@@ -1113,8 +1147,12 @@ PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, con
     uint32_t m[4];
 #if PT_QLINE
     QLine L[kLightSamples];
+    QSlabs SL[kLightSamples];
 #pragma unroll
-    for (int k = 0; k < kLightSamples; ++k) L[k] = q_line(Q, st, T.o32, T.inv[k]);
+    for (int k = 0; k < kLightSamples; ++k) {
+        L[k] = q_line(Q, st, T.o32, T.inv[k]);
+        SL[k] = q_slabs(Q, L[k]);
+    }
 #endif
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -1128,7 +1166,7 @@ PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, con
         for (int k = 0; k < kLightSamples; ++k) {
             // every ray computed, closed ones masked (no per-ray branch)
 #if PT_QLINE
-            const float e0 = q_child_dist(Q, c, L[k], sh->hhi[k]);
+            const float e0 = PT_QDIST(Q, SL[k], c, L[k], sh->hhi[k]);
 #else
             const float e0 = box_dist(l, h, T.inv[k], sh->hhi[k]);
 #endif
@@ -1165,12 +1203,13 @@ PT_HD void ctrav_qnode(ClosestTrav& T, const ClosestStack& K, const SceneK& S, c
     uint32_t m[4];
 #if PT_QLINE
     const QLine L = q_line(Q, st, T.o32, T.inv);
+    const QSlabs SL = q_slabs(Q, L);
 #endif
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         r[c] = Q.ref[c];
 #if PT_QLINE
-        const float e = q_child_dist(Q, c, L, ca->b1);
+        const float e = PT_QDIST(Q, SL, c, L, ca->b1);
 #else
         F3 l, h;
         q_box(Q, c, st, T.o32, &l, &h);
@@ -1285,13 +1324,14 @@ PT_HD void s1_qnode(ShadowTrav1& T, const ShadowStack& K, const SceneK& S, const
     const QNode Q = S.qnode[T.ref];
     const float st[3] = {q_step(Q.ex, 0), q_step(Q.ex, 1), q_step(Q.ex, 2)};
     const QLine L = q_line(Q, st, T.o32, T.inv);
+    const QSlabs SL = q_slabs(Q, L);
     float d[4];
     int rf[4];
     uint32_t m[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         rf[c] = Q.ref[c];
-        const float e = q_child_dist(Q, c, L, r.hhi);
+        const float e = PT_QDIST(Q, SL, c, L, r.hhi);
         d[c] = rf[c] != kNoRef ? e : INFINITY;
     }
     q_sort4(d, rf, m);

@@ -442,15 +442,17 @@ int hc_bvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t*
 // in hc_bvh_check; for every BVH triangle the f64 line meets at sqd, a walk
 // of the QNode tree that enters every child whose test (the kernels'
 // q_child_dist / box_dist) passes within |t| <= sqrt(sqd)(1 + 1e-6) must
-// reach that triangle's leaf.  out: [0] missed hits, [1] hits checked,
-// [2] QNodes.
+// reach that triangle's leaf; the sign-ordered child test the walks use
+// (q_child_dist_s) must equal q_child_dist bit for bit on every child tested.
+// out: [0] missed hits, [1] hits checked, [2] QNodes, [3] child tests whose
+// two forms differ, [4] child tests compared.
 int hc_qbvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t* out) {
     HostScene H;
     if (!prepare_scene(d, &H).empty()) return -1;
     bind_host(&H);
     const SceneK& K = H.k;
-    int64_t missed = 0, checked = 0;
-    if (K.n_qnode == 0) { out[0] = out[1] = 0; out[2] = 0; return 0; }
+    int64_t missed = 0, checked = 0, slab_diff = 0, slab_n = 0;
+    if (K.n_qnode == 0) { out[0] = out[1] = out[2] = out[3] = out[4] = 0; return 0; }
     // leaf of every BVH unit: the leaf codes in the QNode refs
     std::vector<int> leaf_of(K.n_bunit, 0);
     for (int q = 0; q < K.n_qnode; ++q)
@@ -494,11 +496,15 @@ int hc_qbvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t
                     const float step[3] = {q_step(N.ex, 0), q_step(N.ex, 1), q_step(N.ex, 2)};
 #if PT_QLINE
                     const QLine L = q_line(N, step, o32, inv);
+                    const QSlabs SL = q_slabs(N, L);
 #endif
                     for (int c = 0; c < 4; ++c) {
                         if (N.ref[c] == kNoRef) continue;
 #if PT_QLINE
                         const float e = q_child_dist(N, c, L, R);
+                        const float es = q_child_dist_s(SL, c, L, R);
+                        ++slab_n;
+                        if (memcmp(&e, &es, sizeof e) != 0) ++slab_diff;
 #else
                         F3 l, h;
                         q_box(N, c, step, o32, &l, &h);
@@ -511,7 +517,7 @@ int hc_qbvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t
             }
         }
     }
-    out[0] = missed; out[1] = checked; out[2] = K.n_qnode;
+    out[0] = missed; out[1] = checked; out[2] = K.n_qnode; out[3] = slab_diff; out[4] = slab_n;
     return 0;
 }
 

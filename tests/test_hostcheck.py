@@ -170,12 +170,14 @@ def test_bvh_structure_and_conservative_pruning(hostcheck, tmp_path, n_tris, see
 def test_qbvh_walk_conservative(hostcheck, tmp_path, n_tris, seed):
     """The wavefront walks' 4-wide child test (q_child_dist: one fma per slab
     bound on the node grid) never prunes a leaf holding a triangle the f64
-    line meets within range."""
+    line meets within range; its sign-ordered form (q_child_dist_s, the one
+    the walks run) gives the same distance bit for bit."""
     pk = pack_scene(random_scene(tmp_path, n_tris, seed))
-    out = (C.c_int64 * 3)()
+    out = (C.c_int64 * 5)()
     assert hostcheck.hc_qbvh_check(C.byref(pk.desc), C.c_int64(150), C.c_uint64(seed), out) == 0
-    missed, checked, nq = list(out)
+    missed, checked, nq, slab_diff, slab_n = list(out)
     assert nq > 1 and checked > 100 and missed == 0
+    assert slab_n > 1000 and slab_diff == 0   # the walks' sign-ordered child test
 
 
 def test_filter_never_wrong_small_k5(hostcheck, tmp_path):
