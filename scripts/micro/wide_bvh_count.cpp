@@ -57,6 +57,7 @@ struct WTree {
 };
 struct Count { int64_t queries = 0, visits = 0, boxes = 0, leaves = 0, units = 0, mismatches = 0, maxstack = 0; };
 
+int g_order = 0;   // 0: all children nearest-first; 1: the nearest first, the rest in node order
 // children of node q met within R, nearest first
 int wide_children(const WTree& T, int q, F3 o, F3 inv, float R, int32_t* ref, float* d) {
     const WNode& W = T.node[q];
@@ -64,6 +65,12 @@ int wide_children(const WTree& T, int q, F3 o, F3 inv, float R, int32_t* ref, fl
     for (int c = 0; c < W.n; ++c) {
         const float e = cbox_dist(W.lo[c], W.hi[c], o, inv, R);
         if (e < INFINITY) { ref[n] = W.ref[c]; d[n] = e; ++n; }
+    }
+    if (g_order == 1) {   // the nearest to the front, the others keep node order
+        int m = 0;
+        for (int i = 1; i < n; ++i) if (d[i] < d[m]) m = i;
+        for (int j = m; j > 0; --j) { std::swap(d[j], d[j - 1]); std::swap(ref[j], ref[j - 1]); }
+        return n;
     }
     for (int i = 1; i < n; ++i)   // insertion sort, ascending
         for (int j = i; j > 0 && d[j] < d[j - 1]; --j) { std::swap(d[j], d[j - 1]); std::swap(ref[j], ref[j - 1]); }
@@ -141,7 +148,8 @@ void closest_wide(const WTree& T, const SceneK& S, const WfClosestQ& q, ClosestA
 extern "C" {
 // out: for N in {4, 8}: shadow {queries visits boxes leaves units mismatches maxstack}, closest {...}
 // (14 per N), then the shipped walks' stats (8: hc_render_wavefront's walk_stats)
-int wx_count(const pt_scene_desc* d, const pt_render_params* p, int64_t* out) {
+int wx_count(const pt_scene_desc* d, const pt_render_params* p, int64_t* out, int order) {
+    g_order = order;
     HostScene H;
     if (!prepare_scene(d, &H).empty()) return -1;
     bind_host(&H);

@@ -1,5 +1,6 @@
 """Dev experiment: node visits per query of 4- and 8-wide BVH walks on the K5
-scene (wide_bvh_count.cpp, host only).  Usage: wide_bvh_count.py [size] [spp] [n_tris]"""
+scene (wide_bvh_count.cpp, host only).
+Usage: wide_bvh_count.py [size] [spp] [n_tris] [order: 0 nearest-first, 1 nearest then node order]"""
 import ctypes as C
 import json
 import os
@@ -18,6 +19,7 @@ from pathtracerpython_amd.synth import write_k5_scene  # noqa: E402
 size = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 ntri = int(sys.argv[3]) if len(sys.argv) > 3 else 100_000
+order = int(sys.argv[4]) if len(sys.argv) > 4 else 0   # 1: nearest child first, the rest in node order
 so = os.path.join(tempfile.gettempdir(), "wide_bvh_count.so")
 subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-w", "-o", so,
                 os.path.join(HERE, "wide_bvh_count.cpp")], check=True)
@@ -27,11 +29,11 @@ with tempfile.TemporaryDirectory() as d:
     pk = pack_scene(scene_reader.Scene(write_k5_scene(d, n_tris=ntri, seed=0, size=size)))
     p = make_params(size, size, spp, 4, 9, 0)
     out = (C.c_int64 * 36)()
-    rc = lib.wx_count(C.byref(pk.desc), C.byref(p), out)
+    rc = lib.wx_count(C.byref(pk.desc), C.byref(p), out, C.c_int(order))
     assert rc == 0, rc
 o = list(out)
 names = ["queries", "visits", "boxes", "leaves", "units", "mismatches", "maxstack"]
-res = {"size": size, "spp": spp, "n_tris": ntri}
+res = {"size": size, "spp": spp, "n_tris": ntri, "order": order}
 for w, N in enumerate((4, 8)):
     for j, kind in enumerate(("shadow", "closest")):
         v = dict(zip(names, o[w * 14 + j * 7: w * 14 + j * 7 + 7]))
