@@ -3,7 +3,8 @@ pathtracerpython_amd.launch.spawn_ranks exactly as bench.py / the CLI start
 their GPU ranks.  Renders this rank's interleaved row band with the CPU
 oracle (standing in for the HIP tile, which needs a GPU), gathers the tiles to
 rank 0 with distributed.gather_tiles and assembles the frame with
-distributed.deinterleave (the device-side assembly bench.py and the CLI use);
+distributed.deinterleave (equal bands) or distributed.assemble (ragged bands;
+on a GPU both are pt_assemble_bands_device);
 rank 0 saves it to argv[1].  With PT_TEST_FAIL_RANK=r, rank r raises right
 after the rendezvous (the others go on into the gather and block there): the
 fail-fast test of launch.spawn_ranks."""
@@ -19,8 +20,8 @@ import torch.distributed as dist  # noqa: E402
 
 from oracle import oracle  # noqa: E402
 from pathtracerpython_amd import scene_reader  # noqa: E402
-from pathtracerpython_amd.distributed import (band_rows_of, deinterleave, gather_tiles,  # noqa: E402
-                                              max_band_rows)
+from pathtracerpython_amd.distributed import (assemble, band_rows_of, deinterleave,  # noqa: E402
+                                              gather_tiles, max_band_rows)
 from pathtracerpython_amd.launch import pg_timeout, rank_env  # noqa: E402
 from pathtracerpython_amd.pack import pack_scene  # noqa: E402
 
@@ -41,8 +42,11 @@ def main():
     tile[:len(rows)] = torch.from_numpy(cols.reshape(len(rows), W, 3))
     tiles = gather_tiles(tile)
     if rank == 0:
-        frame = deinterleave(torch.stack(tiles), torch.empty((H, W, 3), dtype=torch.float64))
-        np.save(out, frame.numpy())
+        if H % world == 0:   # equal bands: the strided device-style copy
+            frame = deinterleave(torch.stack(tiles), torch.empty((H, W, 3), dtype=torch.float64)).numpy()
+        else:                # ragged bands (pt_assemble_bands_device on a GPU)
+            frame = assemble([t.numpy() for t in tiles], H)
+        np.save(out, frame)
     dist.barrier()
     dist.destroy_process_group()
 

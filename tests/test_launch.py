@@ -1,23 +1,27 @@
 """The self-spawn multi-rank path of bench.py and the CLI (--gpus N /
 --devices N without torch.distributed.run): launch.spawn_ranks starts N fresh
-rank processes with the rendezvous in their environment; here world 2 over
-gloo on CPU, tiles from the oracle (tests/rank_worker.py), device-style
+rank processes with the rendezvous in their environment; here worlds 2 and 8
+over gloo on CPU, tiles from the oracle (tests/rank_worker.py), device-style
 assembly with distributed.deinterleave."""
 import os
 
 import numpy as np
+import pytest
 
 from conftest import ROOT
 
 
-def test_spawn_two_ranks_gloo_frame(tmp_path, packed):
+@pytest.mark.parametrize("world,H", [(2, 12), (8, 16), (8, 13)])
+def test_spawn_ranks_gloo_frame(tmp_path, packed, world, H):
+    """world 8 = the driver's 8-GPU run (here gloo over CPU processes); H = 13:
+    ragged bands of 2 and 1 rows."""
     from oracle import oracle
     from pathtracerpython_amd.launch import spawn_ranks
     from pathtracerpython_amd.render import from_list_order
-    W, H, spp, B, seed = 10, 12, 2, 3, 9   # H a multiple of the world size
+    W, spp, B, seed = 10, 2, 3, 9
     out = str(tmp_path / "frame.npy")
-    rc = spawn_ranks(2, [os.path.join(ROOT, "tests", "rank_worker.py"), out,
-                         str(W), str(H), str(spp), str(B), str(seed)])
+    rc = spawn_ranks(world, [os.path.join(ROOT, "tests", "rank_worker.py"), out,
+                             str(W), str(H), str(spp), str(B), str(seed)])
     assert rc == 0
     full, _ = oracle.render(packed, W, H, spp, B, seed)
     assert np.array_equal(np.load(out), from_list_order(full, W, H))
