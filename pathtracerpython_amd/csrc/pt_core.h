@@ -161,7 +161,8 @@ constexpr int32_t kNoRef = -1;
 struct alignas(16) QNode {
     float org[3];
     uint32_t ex;               // byte a: biased f32 exponent of axis a's grid step
-    uint32_t qlo[3], qhi[3];   // axis a, byte c: child c's bounds in grid steps
+    uint32_t qlo[3], qhi[3];   // axis a, byte c: child c's bounds in grid steps (no child:
+                               // lo 255, hi 0 — an empty box every line misses)
     int32_t ref[4];            // >= 0 QNode, <= -2 leaf (~code), kNoRef: no child
     int32_t pad[2];
 };

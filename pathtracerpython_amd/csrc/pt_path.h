@@ -1078,6 +1078,16 @@ PT_HD QLine q_line(const QNode& Q, const float st[3], F3 o, F3 inv) {
     L.A[2] = st[2] * inv.z; L.B[2] = (Q.org[2] - o.z) * inv.z;
     return L;
 }
+// The same from the node's exponent bytes: A = inv * 2^(byte - 127) is one
+// ldexp (exact, as the product by the power-of-two step is: the builder's
+// bytes are >= 1 and |inv| >= 1, so no result is subnormal).
+PT_HD QLine q_line_ex(const QNode& Q, F3 o, F3 inv) {
+    QLine L;
+    L.A[0] = ldexpf(inv.x, (int)(Q.ex & 0xffu) - 127); L.B[0] = (Q.org[0] - o.x) * inv.x;
+    L.A[1] = ldexpf(inv.y, (int)((Q.ex >> 8) & 0xffu) - 127); L.B[1] = (Q.org[1] - o.y) * inv.y;
+    L.A[2] = ldexpf(inv.z, (int)((Q.ex >> 16) & 0xffu) - 127); L.B[2] = (Q.org[2] - o.z) * inv.z;
+    return L;
+}
 // child c: the smallest |t| of the (two-sided) line inside its box, INFINITY
 // when the box is not met within |t| <= R.  max(tmin, -tmax, 0) is that
 // distance (tmin > 0: tmin; tmax < 0: -tmax; else 0), and the interval meets
@@ -1123,7 +1133,7 @@ PT_HD float q_child_dist_s(const QSlabs& s, int c, const QLine& L, float R) {
 #if PT_QSLABS
 #define PT_QDIST(Q, S, c, L, R) q_child_dist_s((S), (c), (L), (R))
 #else
-#define PT_QDIST(Q, S, c, L, R) q_child_dist((Q), (c), (L), (R))
+#define PT_QDIST(Q, S, c, L, R) ((Q).ref[c] != kNoRef ? q_child_dist((Q), (c), (L), (R)) : INFINITY)
 #endif
 // 4 (distance, ref, rays) triples in ascending distance (sorting network)
 PT_HD void q_sort4(float d[4], int r[4], uint32_t m[4]) {
@@ -1141,7 +1151,6 @@ PT_HD void q_sort4(float d[4], int r[4], uint32_t m[4]) {
 template <bool COUNT>
 PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
     const QNode Q = S.qnode[T.ref];
-    const float st[3] = {q_step(Q.ex, 0), q_step(Q.ex, 1), q_step(Q.ex, 2)};
     float d[4];
     int r[4];
     uint32_t m[4];
@@ -1150,9 +1159,11 @@ PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, con
     QSlabs SL[kLightSamples];
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
-        L[k] = q_line(Q, st, T.o32, T.inv[k]);
+        L[k] = q_line_ex(Q, T.o32, T.inv[k]);
         SL[k] = q_slabs(Q, L[k]);
     }
+#else
+    const float st[3] = {q_step(Q.ex, 0), q_step(Q.ex, 1), q_step(Q.ex, 2)};
 #endif
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -1175,9 +1186,13 @@ PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, con
             dc = fminf(dc, e);
         }
         r[c] = Q.ref[c];
-        const bool live = r[c] != kNoRef && mc != 0;
-        d[c] = live ? dc : INFINITY;
-        m[c] = live ? mc : 0u;
+#if PT_QLINE   // (no child: an empty box, no line meets it)
+        d[c] = dc;
+        m[c] = mc;
+#else
+        d[c] = r[c] != kNoRef ? dc : INFINITY;
+        m[c] = r[c] != kNoRef ? mc : 0u;
+#endif
     }
     q_sort4(d, r, m);
 #pragma unroll
@@ -1197,25 +1212,25 @@ PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, con
 // one 4-wide node of the closest walk
 PT_HD void ctrav_qnode(ClosestTrav& T, const ClosestStack& K, const SceneK& S, const ClosestAcc* ca) {
     const QNode Q = S.qnode[T.ref];
-    const float st[3] = {q_step(Q.ex, 0), q_step(Q.ex, 1), q_step(Q.ex, 2)};
     float d[4];
     int r[4];
     uint32_t m[4];
 #if PT_QLINE
-    const QLine L = q_line(Q, st, T.o32, T.inv);
+    const QLine L = q_line_ex(Q, T.o32, T.inv);
     const QSlabs SL = q_slabs(Q, L);
+#else
+    const float st[3] = {q_step(Q.ex, 0), q_step(Q.ex, 1), q_step(Q.ex, 2)};
 #endif
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         r[c] = Q.ref[c];
 #if PT_QLINE
-        const float e = PT_QDIST(Q, SL, c, L, ca->b1);
+        d[c] = PT_QDIST(Q, SL, c, L, ca->b1);   // (no child: an empty box, INFINITY)
 #else
         F3 l, h;
         q_box(Q, c, st, T.o32, &l, &h);
-        const float e = box_dist(l, h, T.inv, ca->b1);
+        d[c] = r[c] != kNoRef ? box_dist(l, h, T.inv, ca->b1) : INFINITY;
 #endif
-        d[c] = r[c] != kNoRef ? e : INFINITY;
         m[c] = 0;
     }
     q_sort4(d, r, m);
@@ -1322,8 +1337,7 @@ PT_HD int s1_pop(ShadowTrav1& T, const ShadowStack& K, const SceneK& S, const Sh
 // one 4-wide node: nearest child next, the others stacked farthest first
 PT_HD void s1_qnode(ShadowTrav1& T, const ShadowStack& K, const SceneK& S, const Shadow1& r) {
     const QNode Q = S.qnode[T.ref];
-    const float st[3] = {q_step(Q.ex, 0), q_step(Q.ex, 1), q_step(Q.ex, 2)};
-    const QLine L = q_line(Q, st, T.o32, T.inv);
+    const QLine L = q_line_ex(Q, T.o32, T.inv);
     const QSlabs SL = q_slabs(Q, L);
     float d[4];
     int rf[4];
@@ -1331,8 +1345,7 @@ PT_HD void s1_qnode(ShadowTrav1& T, const ShadowStack& K, const SceneK& S, const
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         rf[c] = Q.ref[c];
-        const float e = PT_QDIST(Q, SL, c, L, r.hhi);
-        d[c] = rf[c] != kNoRef ? e : INFINITY;
+        d[c] = PT_QDIST(Q, SL, c, L, r.hhi);   // (no child: an empty box, INFINITY)
     }
     q_sort4(d, rf, m);
 #pragma unroll

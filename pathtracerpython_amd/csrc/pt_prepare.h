@@ -201,6 +201,7 @@ struct QBuilder {
                 hi |= (uint32_t)qh << (8 * c);
             }
             if (!ok) continue;
+            for (int c = n; c < 4; ++c) lo |= 255u << (8 * c);   // no child: an empty box
             Q->org[a] = (float)org;
             Q->ex |= (uint32_t)(e + 127) << (8 * a);
             Q->qlo[a] = lo;

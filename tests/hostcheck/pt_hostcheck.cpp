@@ -443,7 +443,8 @@ int hc_bvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t*
 // of the QNode tree that enters every child whose test (the kernels'
 // q_child_dist / box_dist) passes within |t| <= sqrt(sqd)(1 + 1e-6) must
 // reach that triangle's leaf; the sign-ordered child test the walks use
-// (q_child_dist_s) must equal q_child_dist bit for bit on every child tested.
+// (q_child_dist_s, on q_line_ex's slab parameters) must equal q_child_dist
+// bit for bit on every child tested, and reject every absent child.
 // out: [0] missed hits, [1] hits checked, [2] QNodes, [3] child tests whose
 // two forms differ, [4] child tests compared.
 int hc_qbvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t* out) {
@@ -498,8 +499,14 @@ int hc_qbvh_check(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, int64_t
                     const QLine L = q_line(N, step, o32, inv);
                     const QSlabs SL = q_slabs(N, L);
 #endif
+                    const QLine LX = q_line_ex(N, o32, inv);
+                    if (memcmp(&LX, &L, sizeof L) != 0) ++slab_diff;   // the walks' ldexp form
                     for (int c = 0; c < 4; ++c) {
-                        if (N.ref[c] == kNoRef) continue;
+                        if (N.ref[c] == kNoRef) {   // an empty box: no line meets it
+                            ++slab_n;
+                            if (q_child_dist_s(SL, c, L, INFINITY) != INFINITY) ++slab_diff;
+                            continue;
+                        }
 #if PT_QLINE
                         const float e = q_child_dist(N, c, L, R);
                         const float es = q_child_dist_s(SL, c, L, R);
