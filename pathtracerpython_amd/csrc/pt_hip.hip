@@ -484,7 +484,7 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
     // (4 B each per lane), the rest in global memory
     __shared__ int stack[kWalkStackLds][256];
     const int lanes = (int)gridDim.x * 256, gl = (int)(blockIdx.x * 256u + threadIdx.x);
-    const ShadowStack K{&stack[0][threadIdx.x], 256, ovf + gl, lanes, kWalkStackLds};
+    const ShadowStackLds K{(PT_LDS int*)&stack[0][threadIdx.x], 256, ovf + gl, lanes, kWalkStackLds};
     Shadow1 r;
     ShadowTrav1 T;
     T.ref = kNoRef;
@@ -571,7 +571,8 @@ __global__ __launch_bounds__(256, PT_CLOSEST_WAVES) void k_wf_closest(SceneK S, 
     __shared__ int sref[kWalkStackLds][256];
     __shared__ uint16_t sdist[kWalkStackLds][256];
     const int lanes = (int)gridDim.x * 256, gl = (int)(blockIdx.x * 256u + threadIdx.x);
-    const ClosestStack K{&sref[0][threadIdx.x], &sdist[0][threadIdx.x], 256, ovf_ref + gl,
+    const ClosestStackLds K{(PT_LDS int*)&sref[0][threadIdx.x], (PT_LDS uint16_t*)&sdist[0][threadIdx.x], 256,
+                            ovf_ref + gl,
                          ovf_dist + gl, lanes, kWalkStackLds};
     T.ref = kNoRef;
     int pl = kNoRef, pl2 = kNoRef;   // postponed leaves

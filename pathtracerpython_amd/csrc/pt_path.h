@@ -772,9 +772,19 @@ struct ClosestTrav {
 // non-negative float rounds down, so the pop check against the shrinking
 // bound is conservative: it may visit a node the exact distance would skip,
 // never the reverse).
-struct ClosestStack {
-    int* ref;
-    uint16_t* dist;
+// PT_LDS: the walk kernels' stacks live in shared memory.  Their views name
+// that address space, so pushes and pops compile to LDS instructions: through
+// generic pointers the compiler merged each LDS store with its rare global
+// overflow store into one flat store on a selected address.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PT_LDS __attribute__((address_space(3)))
+#else
+#define PT_LDS
+#endif
+template <class R, class D>   // R: int* / PT_LDS int*, D: uint16_t* / PT_LDS uint16_t*
+struct ClosestStackT {
+    R ref;
+    D dist;
     int stride;
     // the walk kernels keep the first nl entries in LDS (ref / dist, stride
     // `stride`) and the deeper ones, rarely touched, in global memory (gref /
@@ -790,6 +800,8 @@ struct ClosestStack {
     PT_HD int get_ref(int i) const { return i < nl ? ref[i * stride] : gref[(i - nl) * gs]; }
     PT_HD uint16_t get_dist(int i) const { return i < nl ? dist[i * stride] : gdist[(i - nl) * gs]; }
 };
+using ClosestStack = ClosestStackT<int*, uint16_t*>;
+using ClosestStackLds = ClosestStackT<PT_LDS int*, PT_LDS uint16_t*>;
 struct ClosestStackLocal {
     int ref[kBvhStack];
     uint16_t dist[kBvhStack];
@@ -806,7 +818,8 @@ PT_HD float dist_up16(uint16_t h) {
     memcpy(&d, &b, sizeof d);
     return d;
 }
-PT_HD void ctrav_push(ClosestTrav& T, const ClosestStack& K, int r, float d) {
+template <class KS>
+PT_HD void ctrav_push(ClosestTrav& T, const KS& K, int r, float d) {
     if (T.tref != kNoRef) {
         K.set(T.top, T.tref, dist_down16(T.tdist));
         ++T.top;
@@ -814,7 +827,8 @@ PT_HD void ctrav_push(ClosestTrav& T, const ClosestStack& K, int r, float d) {
     T.tref = r;
     T.tdist = d;
 }
-PT_HD int ctrav_pop(ClosestTrav& T, const ClosestStack& K, float bound) {   // next node within the bound, or kNoRef
+template <class KS>
+PT_HD int ctrav_pop(ClosestTrav& T, const KS& K, float bound) {   // next node within the bound, or kNoRef
     while (T.tref != kNoRef) {
         const int r = T.tref;
         const float d = T.tdist;
@@ -888,8 +902,8 @@ PT_HD void ctrav_units(const ClosestTrav& T, const SceneK& S, ClosestAcc* ca, co
     }
 }
 // the leaf T.ref, then the next entry
-template <bool COUNT, bool UC = false>
-PT_HD void ctrav_leaf(ClosestTrav& T, const ClosestStack& K, const SceneK& S, ClosestAcc* ca,
+template <bool COUNT, bool UC = false, class KS = ClosestStack>
+PT_HD void ctrav_leaf(ClosestTrav& T, const KS& K, const SceneK& S, ClosestAcc* ca,
                       const Spill& sp, Counters* cnt) {
     ctrav_units<COUNT, UC>(T, S, ca, sp, cnt, T.ref);
     T.ref = ctrav_pop(T, K, ca->b1);
@@ -930,8 +944,9 @@ struct ShadowTrav {
 };
 // a strided view: a per-lane local array (stride 1, scratch memory) or a
 // column of a shared-memory array (stride = block size; the walk kernels)
-struct ShadowStack {
-    int* e;
+template <class E>   // int* / PT_LDS int*
+struct ShadowStackT {
+    E e;
     int stride;
     // entries from nl on in global memory (g, stride gs): see ClosestStack
     int* g = nullptr;
@@ -943,6 +958,8 @@ struct ShadowStack {
         else g[(i - nl) * gs] = v;
     }
 };
+using ShadowStack = ShadowStackT<int*>;
+using ShadowStackLds = ShadowStackT<PT_LDS int*>;
 template <bool COUNT>
 PT_HD int strav_pop(ShadowTrav& T, const ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
     const uint32_t open = shadow_open<COUNT>(S, sh);
@@ -1210,7 +1227,8 @@ PT_HD void strav_qnode(ShadowTrav& T, const ShadowStack& K, const SceneK& S, con
     }
 }
 // one 4-wide node of the closest walk
-PT_HD void ctrav_qnode(ClosestTrav& T, const ClosestStack& K, const SceneK& S, const ClosestAcc* ca) {
+template <class KS>
+PT_HD void ctrav_qnode(ClosestTrav& T, const KS& K, const SceneK& S, const ClosestAcc* ca) {
     const QNode Q = S.qnode[T.ref];
     float d[4];
     int r[4];
@@ -1328,14 +1346,16 @@ PT_HD void s1_init(ShadowTrav1& T, const SceneK& S, F3 o32, int ogrp, const Shad
     T.ref = (shadow1_open(S, r) && box_hit(l, h, T.inv, r.hhi)) ? root : kNoRef;
 }
 // next stacked entry, or kNoRef when the ray is closed or the stack empty
-PT_HD int s1_pop(ShadowTrav1& T, const ShadowStack& K, const SceneK& S, const Shadow1& r) {
+template <class KS>
+PT_HD int s1_pop(ShadowTrav1& T, const KS& K, const SceneK& S, const Shadow1& r) {
     if (!shadow1_open(S, r)) return kNoRef;
     const int e = T.tc;
     T.tc = T.top > 0 ? K.get(--T.top) : kNoRef;
     return e;
 }
 // one 4-wide node: nearest child next, the others stacked farthest first
-PT_HD void s1_qnode(ShadowTrav1& T, const ShadowStack& K, const SceneK& S, const Shadow1& r) {
+template <class KS>
+PT_HD void s1_qnode(ShadowTrav1& T, const KS& K, const SceneK& S, const Shadow1& r) {
     const QNode Q = S.qnode[T.ref];
     const QLine L = q_line_ex(Q, T.o32, T.inv);
     const QSlabs SL = q_slabs(Q, L);
