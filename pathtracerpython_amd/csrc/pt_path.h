@@ -802,9 +802,12 @@ struct ClosestStackT {
 };
 using ClosestStack = ClosestStackT<int*, uint16_t*>;
 using ClosestStackLds = ClosestStackT<PT_LDS int*, PT_LDS uint16_t*>;
+// (local stacks hold kBvhStack + 2 entries: push3's dead stores reach two
+// entries above the deepest live one)
+constexpr int kBvhStackLocal = kBvhStack + 2;
 struct ClosestStackLocal {
-    int ref[kBvhStack];
-    uint16_t dist[kBvhStack];
+    int ref[kBvhStackLocal];
+    uint16_t dist[kBvhStackLocal];
     PT_HD ClosestStack view() { return ClosestStack{ref, dist, 1}; }
 };
 PT_HD uint16_t dist_down16(float d) {
@@ -817,6 +820,35 @@ PT_HD float dist_up16(uint16_t h) {
     float d;
     memcpy(&d, &b, sizeof d);
     return d;
+}
+// The pushes of a 4-wide node visit (children 3, 2, 1 of the distance order,
+// farthest first; v1 >= v2 >= v3 since misses sort last) onto a stack with
+// its top entry cached in (tc, td): what ctrav_push does child by child, but
+// when the three entries fit below nl as unconditional stores above the top,
+// each advancing the top only when its entry is real — no branch per child.
+// (Stores at or above the final top are dead entries.)
+template <class KS>
+PT_HD void push3(const KS& K, int& top, int& tc, float& td, bool v1, bool v2, bool v3, int r1, float d1,
+                 int r2, float d2, int r3, float d3) {
+    if (top + 3 <= K.nl) {
+        int p = top;
+        K.ref[p * K.stride] = tc;
+        K.dist[p * K.stride] = dist_down16(td);
+        p += (v1 && tc != kNoRef) ? 1 : 0;
+        K.ref[p * K.stride] = r3;
+        K.dist[p * K.stride] = dist_down16(d3);
+        p += v3 ? 1 : 0;
+        K.ref[p * K.stride] = r2;
+        K.dist[p * K.stride] = dist_down16(d2);
+        p += v2 ? 1 : 0;
+        top = p;
+    } else {
+        if (v1 && tc != kNoRef) K.set(top++, tc, dist_down16(td));
+        if (v3) K.set(top++, r3, dist_down16(d3));
+        if (v2) K.set(top++, r2, dist_down16(d2));
+    }
+    tc = v1 ? r1 : tc;
+    td = v1 ? d1 : td;
 }
 template <class KS>
 PT_HD void ctrav_push(ClosestTrav& T, const KS& K, int r, float d) {
@@ -960,6 +992,28 @@ struct ShadowStackT {
 };
 using ShadowStack = ShadowStackT<int*>;
 using ShadowStackLds = ShadowStackT<PT_LDS int*>;
+// push3 for the one-ray shadow walk's stack (refs only)
+template <class KS>
+PT_HD void push3_ref(const KS& K, int& top, int& tc, bool v1, bool v2, bool v3, int r1, int r2, int r3) {
+    if (top + 3 <= K.nl) {
+        int p = top;
+        K.e[p * K.stride] = tc;
+        p += (v1 && tc != kNoRef) ? 1 : 0;
+        K.e[p * K.stride] = r3;
+        p += v3 ? 1 : 0;
+        K.e[p * K.stride] = r2;
+        p += v2 ? 1 : 0;
+        top = p;
+    } else {
+        if (v1 && tc != kNoRef) K.set(top++, tc);
+        if (v3) K.set(top++, r3);
+        if (v2) K.set(top++, r2);
+    }
+    tc = v1 ? r1 : tc;
+}
+#ifndef PT_PUSH3
+#define PT_PUSH3 1
+#endif
 template <bool COUNT>
 PT_HD int strav_pop(ShadowTrav& T, const ShadowStack& K, const SceneK& S, const ShadowSet* sh) {
     const uint32_t open = shadow_open<COUNT>(S, sh);
@@ -1163,6 +1217,33 @@ PT_HD void q_sort4(float d[4], int r[4], uint32_t m[4]) {
     };
     cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
 }
+// 4 (distance, ref) pairs in ascending distance: q_sort4's network and tie
+// order (an exchange only when d[j] < d[i]; d is >= 0 or +inf, so its bit
+// pattern orders as the float does) on the pairs packed as 64-bit words.
+// Through q_sort4 the compiler tracked the refs as a permutation of the four
+// loaded words and rebuilt each with a chain of index compares.
+PT_HD uint32_t f32_bits(float x) { uint32_t b; memcpy(&b, &x, 4); return b; }
+PT_HD float bits_f32(uint32_t b) { float x; memcpy(&x, &b, 4); return x; }
+PT_HD void q_sort4_pairs(float d[4], int r[4]) {
+    uint64_t k[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) k[c] = ((uint64_t)f32_bits(d[c]) << 32) | (uint32_t)r[c];
+    auto cs = [&](int i, int j) {
+        const uint64_t a = k[i], b = k[j];
+        const bool sw = (uint32_t)(b >> 32) < (uint32_t)(a >> 32);
+        k[i] = sw ? b : a;
+        k[j] = sw ? a : b;
+    };
+    cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        d[c] = bits_f32((uint32_t)(k[c] >> 32));
+        r[c] = (int)(uint32_t)k[c];
+    }
+}
+#ifndef PT_QSORT_PAIRS
+#define PT_QSORT_PAIRS 1
+#endif
 // one 4-wide node of the shadow walk (T.ref >= 0 a QNode): nearest child
 // next, the others stacked farthest first
 template <bool COUNT>
@@ -1232,7 +1313,9 @@ PT_HD void ctrav_qnode(ClosestTrav& T, const KS& K, const SceneK& S, const Close
     const QNode Q = S.qnode[T.ref];
     float d[4];
     int r[4];
-    uint32_t m[4];
+#if !PT_QSORT_PAIRS
+    uint32_t m[4] = {0u, 0u, 0u, 0u};
+#endif
 #if PT_QLINE
     const QLine L = q_line_ex(Q, T.o32, T.inv);
     const QSlabs SL = q_slabs(Q, L);
@@ -1249,12 +1332,20 @@ PT_HD void ctrav_qnode(ClosestTrav& T, const KS& K, const SceneK& S, const Close
         q_box(Q, c, st, T.o32, &l, &h);
         d[c] = r[c] != kNoRef ? box_dist(l, h, T.inv, ca->b1) : INFINITY;
 #endif
-        m[c] = 0;
     }
+#if PT_QSORT_PAIRS
+    q_sort4_pairs(d, r);
+#else
     q_sort4(d, r, m);
+#endif
+#if PT_PUSH3
+    push3(K, T.top, T.tref, T.tdist, d[1] < INFINITY, d[2] < INFINITY, d[3] < INFINITY, r[1], d[1], r[2], d[2],
+          r[3], d[3]);
+#else
 #pragma unroll
     for (int c = 3; c >= 1; --c)
         if (d[c] < INFINITY) ctrav_push(T, K, r[c], d[c]);
+#endif
     T.ref = d[0] < INFINITY ? r[0] : ctrav_pop(T, K, ca->b1);
 }
 
@@ -1361,13 +1452,22 @@ PT_HD void s1_qnode(ShadowTrav1& T, const KS& K, const SceneK& S, const Shadow1&
     const QSlabs SL = q_slabs(Q, L);
     float d[4];
     int rf[4];
+#if !PT_QSORT_PAIRS
     uint32_t m[4] = {0u, 0u, 0u, 0u};
+#endif
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         rf[c] = Q.ref[c];
         d[c] = PT_QDIST(Q, SL, c, L, r.hhi);   // (no child: an empty box, INFINITY)
     }
+#if PT_QSORT_PAIRS
+    q_sort4_pairs(d, rf);
+#else
     q_sort4(d, rf, m);
+#endif
+#if PT_PUSH3
+    push3_ref(K, T.top, T.tc, d[1] < INFINITY, d[2] < INFINITY, d[3] < INFINITY, rf[1], rf[2], rf[3]);
+#else
 #pragma unroll
     for (int c = 3; c >= 1; --c) {
         if (d[c] < INFINITY) {
@@ -1375,6 +1475,7 @@ PT_HD void s1_qnode(ShadowTrav1& T, const KS& K, const SceneK& S, const Shadow1&
             T.tc = rf[c];
         }
     }
+#endif
     T.ref = d[0] < INFINITY ? rf[0] : s1_pop(T, K, S, r);
 }
 // the units of leaf `ref` (<= -2)

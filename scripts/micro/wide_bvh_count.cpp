@@ -206,7 +206,7 @@ int wx_count(const pt_scene_desc* d, const pt_render_params* p, int64_t* out, in
                 wf_get_shadow1(SQ[i], k, &o32, &ogrp, &r);
                 const Shadow1 r0 = r;
                 ShadowTrav1 T;
-                int buf[kBvhStack];
+                int buf[kBvhStackLocal];
                 const ShadowStack K{buf, 1};
                 s1_init(T, H.k, o32, ogrp, r, H.k.qroot);
                 ++ws[0];

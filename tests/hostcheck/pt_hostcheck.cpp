@@ -174,7 +174,7 @@ int hc_render_wavefront2(const pt_scene_desc* d, const pt_render_params* p, doub
                 int ogrp;
                 wf_get_shadow1(SQ[i], k, &o32, &ogrp, &r);
                 ShadowTrav1 T;
-                int buf[kBvhStack];
+                int buf[kBvhStackLocal];
                 const ShadowStack K{buf, 1};
                 s1_init(T, H.k, o32, ogrp, r, H.k.qroot);
                 ++ws[0];
