@@ -21,8 +21,9 @@ spp = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 ntri = int(sys.argv[3]) if len(sys.argv) > 3 else 100_000
 order = int(sys.argv[4]) if len(sys.argv) > 4 else 0   # 1: nearest child first, the rest in node order
 so = os.path.join(tempfile.gettempdir(), "wide_bvh_count.so")
+# WX_FLAGS: extra compiler flags (builder variants, e.g. -DPT_BVH_BINS=64)
 subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-w", "-o", so,
-                os.path.join(HERE, "wide_bvh_count.cpp")], check=True)
+                os.path.join(HERE, "wide_bvh_count.cpp")] + os.environ.get("WX_FLAGS", "").split(), check=True)
 lib = C.CDLL(so)
 scene_reader.VERBOSE = False
 with tempfile.TemporaryDirectory() as d:
