@@ -152,15 +152,19 @@ def k5(tmp_path_factory):
 def test_k5_full(k5):
     """K5: 100k-triangle synthetic mesh, 1024x1024, 256 spp, 4 bounces (the
     wavefront path, ~2 s).  Oracle (brute force over all triangles) on 16
-    pixels over bottom, middle and top rows; finite everywhere; a 64x64
-    render of the same scene is bitwise equal between the wavefront, the
-    single kernel and the forced-f64 kernel."""
+    pixels over bottom, middle and top rows; finite everywhere; the whole
+    frame bitwise equal to the single kernel's (a different traversal of the
+    same BVH: packet shadow walks, ~7 s); a 64x64 render of the same scene is
+    bitwise equal between the wavefront, the single kernel and the forced-f64
+    kernel."""
     W = H = 1024
     with Renderer(k5) as r:
         packed = r.packed
         assert r.packed.n_tri == 100_012
         fb = render_dev(r, r.params(W, H, 256, 4, 9, out_f64=True))
         assert np.isfinite(fb).all()
+        mk = render_dev(r, r.params(W, H, 256, 4, 9, out_f64=True, megakernel=True))
+        assert np.array_equal(fb, mk), np.abs(fb - mk).max()
         small = r.render(64, 64, 2, 4, 9, out_f64=True)
         assert np.array_equal(small, r.render(64, 64, 2, 4, 9, out_f64=True, megakernel=True))
         assert np.array_equal(small, r.render(64, 64, 2, 4, 9, out_f64=True, force_f64=True))
