@@ -205,6 +205,10 @@ struct SceneK {
                                  // coplanar pair or degenerate: the walks read bunit)
     float bvh_eh, bvh_eq, bvh_qhi;   // maxima over bunit
     int32_t bvh_obj1;            // the BVH's one object, or -1 (several: from tri_obj)
+    const float* unit_lc;        // [2 n_obj_unit] light-side cull thresholds of `unit`
+                                 // (pt_prepare.h light_cull): a shadow ray from an origin
+                                 // whose f32 plane value h has h > lc[0] or h < lc[1]
+                                 // certainly misses the unit, whichever light point it takes
 };
 
 // ------------------------------------------------------------------ RNG --

@@ -750,6 +750,19 @@ static int dev_alloc_copy(T** d, const T* h, size_t n) {
     return PT_OK;
 }
 
+#if defined(PT_SKIPSTAT)
+// dev builds only (scripts/skip_stats.py): the unit-pass skip counters of pt_path.h
+extern "C" int pt_debug_skip_stats(unsigned long long* out, int reset) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(pt_skip_stat), 16 * sizeof(unsigned long long)));
+    if (reset) {
+        unsigned long long z[16] = {};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pt_skip_stat), z, sizeof(z)));
+    }
+    return PT_OK;
+}
+#endif
+
 #if defined(PT_PHASE_CLOCKS)
 // dev builds only (scripts/phase_clocks.py): the phase clocks of pt_path.h
 extern "C" int pt_debug_phase_clocks(unsigned long long* out, int reset) {
@@ -830,7 +843,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         if (prop.multiProcessorCount > 0) s->n_cu = prop.multiProcessorCount;
     }
     HostScene& H = s->host;
-    constexpr int kArrays = 14;
+    constexpr int kArrays = 15;
     const size_t sz[kArrays] = {H.unit.size() * sizeof(UnitF), H.trid.size() * sizeof(TriD),
                                 H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
                                 H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
@@ -838,11 +851,12 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
                                 H.tri_grp.size() * sizeof(int32_t),
                                 H.bnode.size() * sizeof(BNode), H.bunit.size() * sizeof(UnitF),
                                 H.cnode.size() * sizeof(CNode), H.qnode.size() * sizeof(QNode),
-                                H.bunitc.size() * sizeof(UnitC), H.unit_eye.size() * sizeof(UnitF)};
+                                H.bunitc.size() * sizeof(UnitC), H.unit_eye.size() * sizeof(UnitF),
+                                H.unit_lc.size() * sizeof(float)};
     const void* src[kArrays] = {H.unit.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
                                 H.mat.data(), H.light_tri.data(), H.light_cum.data(),
                                 H.tri_grp.data(), H.bnode.data(), H.bunit.data(), H.cnode.data(),
-                                H.qnode.data(), H.bunitc.data(), H.unit_eye.data()};
+                                H.qnode.data(), H.bunitc.data(), H.unit_eye.data(), H.unit_lc.data()};
     size_t off[kArrays], total = 0;
     for (int i = 0; i < kArrays; ++i) { off[i] = total; total += align_up(sz[i]); }
     int rc = PT_OK;
@@ -871,6 +885,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     s->dev.qnode = (const QNode*)(b + off[11]);
     s->dev.bunitc = H.bunitc.empty() ? nullptr : (const UnitC*)(b + off[12]);
     s->dev.unit_eye = (const UnitF*)(b + off[13]);
+    s->dev.unit_lc = (const float*)(b + off[14]);
     s->xb_surf = box_bound(H, false);
     s->xb_all = box_bound(H, true);
     *out = s;

@@ -290,6 +290,43 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double u[12], ShadowS
 #ifndef PT_QUAD
 #define PT_QUAD 1
 #endif
+// Experiment switches (both exact, both measured
+// slower — 5.68 / 5.70 vs 5.62 ms — so both are off): the light-side cull of
+// the uniform units' shadow tests, and the closest ray's skip of a unit
+// certainly beyond the current winner.  Wave-level counts from a
+// -DPT_SKIPSTAT build (scripts/skip_stats.py): the cull removes 19% of the
+// shadow parts (lane level: 62% of (lane, unit) pairs), the closest skip 2.4%.
+#ifndef PT_LCULL
+#define PT_LCULL 0
+#endif
+#ifndef PT_CSKIP
+#define PT_CSKIP 0
+#endif
+// a lower bound any test of a unit could add (f32: at - dt; f64 fallback:
+// sqrtf(sqd)(1 - 1e-6) >= (at - dt)(1 - 1.2e-6)) is above (at - dt) kCSkip
+constexpr float kCSkip = 1.0f - 4e-6f;
+#if defined(PT_SKIPSTAT) && defined(__HIP__)
+__device__ unsigned long long pt_skip_stat[16];   // (dev builds: the host reads it)
+#endif
+#if defined(PT_SKIPSTAT) && defined(__HIP_DEVICE_COMPILE__)
+// one count per wave (its first active lane) when the wave-uniform c holds
+#define PT_SKIP_EV(i, c)                                                          \
+    do {                                                                          \
+        const bool c_ = (c);                                                      \
+        if (c_ && __lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1)    \
+            atomicAdd(&pt_skip_stat[(i)], 1ull);                                  \
+    } while (0)
+// the number of the wave's active lanes where c holds
+#define PT_SKIP_LANES(i, c)                                                       \
+    do {                                                                          \
+        const unsigned long long b_ = __ballot((c));                              \
+        if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1)          \
+            atomicAdd(&pt_skip_stat[(i)], (unsigned long long)__popcll(b_));      \
+    } while (0)
+#else
+#define PT_SKIP_EV(i, c)
+#define PT_SKIP_LANES(i, c)
+#endif
 #ifndef PT_RNG_PERBLOCK
 #define PT_RNG_PERBLOCK 1
 #endif
@@ -374,6 +411,11 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
         const RayPlane p = ray_plane(U, O.h, d, sh->hlo[k], sh->hhi[k]);
         float cm, nm;
         margin_plane(U, p, sh->hlo[k], sh->hhi[k], cop, &cm, &nm);
+#if defined(PT_SKIPSTAT)
+        PT_SKIP_EV(3 + k, true);
+        PT_SKIP_EV(6 + k, !PT_WAVE_ANY(!(nm < 0.0f)));
+        PT_SKIP_LANES(13 + k, nm < 0.0f || (k < 2 && oc[k] > 0.0f));
+#endif
         // nm < 0 (the plane part is a certain miss; nm is never NaN, cop is
         // not) implies cm < 0, so every margin of the ray's triangles is
         // negative or a dropped NaN: no occlusion, no ambiguous test.  The
@@ -543,7 +585,7 @@ template <bool FORCE64, bool COUNT, bool MARGIN = false, int PARTS = 3>
 PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
                       bool do_shadow, bool do_closest, ShadowSet* sh, F3 n32, ClosestAcc* ca,
                       const Spill& sp, Counters* cnt, uint32_t rays = 15u,
-                      float* oc = nullptr) {
+                      float* oc = nullptr, bool ctrace = true) {
     if (!(PARTS & 1)) do_shadow = false;
     if (!(PARTS & 2)) do_closest = false;
     // rays: bit k = shadow ray k, bit 3 = the closest ray (the BVH passes the
@@ -592,6 +634,22 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
     }
     if (!FORCE64 && do_closest && (rays & 8u)) {
         const RayPlane p = ray_plane(U, O.h, n32, INFINITY, INFINITY);
+#if defined(PT_SKIPSTAT)
+        if (MARGIN) {
+            PT_SKIP_EV(9, true);
+            PT_SKIP_EV(10, !PT_WAVE_ANY(ctrace && !((p.at - p.dt) * kCSkip > ca->b1)));
+        }
+#endif
+#if PT_CSKIP
+        // the unit cannot change the closest-hit decision when its |t| is
+        // certainly beyond the current winner's upper bound b1 (every lower
+        // bound a test of it could add, an f64 fallback's included, exceeds
+        // b1: neither the winner nor the certainty test b1 < a2 changes,
+        // closest_add / closest_finish); skipped when that holds on every
+        // lane that traces
+        if (MARGIN && !PT_WAVE_ANY(ctrace && !((p.at - p.dt) * kCSkip > ca->b1))) goto closest_done;
+#endif
+        {
         bool c0, a0, c1 = false, a1 = false;
         if (MARGIN && PT_QUAD) {   // the render loop's unit form (quad_m)
             const QuadM m = quad_m(U, p, O, n32);
@@ -616,7 +674,11 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
         closest_add(ca, c0 ? U.t[0] : U.t[1], c ? p.at - p.dt : INFINITY,
                     c ? p.at + p.dt : INFINITY);
         amb |= (a0 ? 64u : 0u) | (a1 ? 128u : 0u);
+        }
     }
+#if PT_CSKIP
+closest_done:
+#endif
 #ifdef PT_ABL_NOAMB   // timing ablation only (wrong results)
     if (!FORCE64) amb = 0;
 #endif
@@ -1746,11 +1808,36 @@ PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& 
 #ifdef PT_ABL_NOSHADOW   // timing ablation only (wrong results)
                 const bool do_shadow = false;
 #else
+#if PT_LCULL
+                // a lane needs no shadow test of this unit when its three rays
+                // are occluded (ray 2: by an object <= this one, scene order),
+                // its origin is on the unit's plane (certain misses) or the
+                // light-side cull holds for every light point (pt_prepare.h
+                // light_cull): the wave skips the unit's shadow part,
+                // plane parts included, when no lane needs it
+                const float lc0 = S.unit_lc[2 * u], lc1 = S.unit_lc[2 * u + 1];
+                const bool lane_off = (oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f) |
+                                      (U.grp == ogrp) | (O.h > lc0) | (O.h < lc1);
+                const bool do_shadow = PT_WAVE_ANY(!lane_off);
+#else
                 const bool do_shadow =
                     PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));
 #endif
+#if defined(PT_SKIPSTAT)
+                {
+                    const float lc0s = S.unit_lc[2 * u], lc1s = S.unit_lc[2 * u + 1];
+                    PT_SKIP_EV(0, true);
+                    PT_SKIP_EV(1, PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f)));
+                    PT_SKIP_EV(2, PT_WAVE_ANY(!((oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f) |
+                                                (U.grp == ogrp) | (O.h > lc0s) | (O.h < lc1s))));
+                    PT_SKIP_LANES(11, true);
+                    PT_SKIP_LANES(12, (oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f) |
+                                          (U.grp == ogrp) | (O.h > lc0s) | (O.h < lc1s));
+                }
+#endif
+#endif
                 fused_unit<FORCE64, COUNT, true>(S, U, O, U.grp == ogrp, do_shadow, any_trace,
-                                                 &sh, n32, &ca, sp, cnt, 15u, oc);
+                                                 &sh, n32, &ca, sp, cnt, 15u, oc, trace);
             }
 #pragma unroll
             for (int k = 0; k < kLightSamples; ++k) sh.occ[k] = oc[k] > 0.0f;

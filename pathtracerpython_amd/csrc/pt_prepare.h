@@ -31,6 +31,7 @@ struct HostScene {
     std::vector<Mat> mat;
     std::vector<int32_t> light_tri;
     std::vector<double> light_cum;
+    std::vector<float> unit_lc;   // [2 n_obj_unit] light_cull thresholds
     SceneK k{};   // pointers unset; constants filled
 };
 
@@ -353,6 +354,54 @@ inline float f32_up(double x) {   // round to f32, never below x (x >= 0)
     float f = (float)x;
     if ((double)f < x) f = nextafterf(f, INFINITY);
     return f;
+}
+
+// Light-side cull of the uniform units' shadow tests (render loop,
+// pt_path.h).  A shadow ray from P toward a light point L is the line
+// P + s (L - P), |s| < 1 (main.py:37-47: two-sided, squared distance below
+// |L - P|^2).  Let h be a member triangle's signed plane distance (its
+// reference plane, utils.py:109-111).  If every light vertex has h > m1 (the
+// light strictly on the positive side: so has every sampled L, a convex
+// combination) and h(P) > max_L h / 2 + m2, the line meets the plane at
+// s = h(P) / (h(P) - h(L)) with |s| - 1 >= min(m1 / h(P), 2 m2 / max h) > 0:
+// beyond L (h(L) < h(P)) or behind P farther than |L - P| (h(L) > h(P)),
+// certainly outside the reference's range for every light sample.  The
+// negative side is symmetric.  The kernel's f32 h(P) (origin_q, surface
+// frame) errs by at most U.eh from each member's h, so the thresholds
+// include eh and round outward:
+//   lc[0] = up(max h / 2 + m2 + eh)  (h > lc[0]: cull), +inf when no cull
+//   lc[1] = down(min h / 2 - m2 - eh) (h < lc[1]: cull), -inf when no cull
+// m1 = m2 = 1e-6 (relative margin >= ~1e-8 against the reference's own f64
+// rounding of t and of the squared distances, ~1e-11 even for grazing lines).
+inline void light_cull(HostScene* H, const pt_scene_desc* d) {
+    const int T = d->n_tri;
+    const double m1 = 1e-6, m2 = 1e-6;
+    H->unit_lc.assign(2 * (size_t)H->k.n_obj_unit, 0.f);
+    for (int u = 0; u < H->k.n_obj_unit; ++u) {
+        const UnitF& U = H->unit[u];
+        float* lc = &H->unit_lc[2 * (size_t)u];
+        lc[0] = INFINITY;
+        lc[1] = -INFINITY;
+        if (!(U.eh >= 0.f) || !(U.eh < 1e30f) || d->n_obj_tri >= T) continue;   // degenerate / no light
+        double hmin = INFINITY, hmax = -INFINITY;
+        for (int m = 0; m < U.count; ++m) {
+            const TriD& E = H->trid[U.t[m]];
+            for (int lt = d->n_obj_tri; lt < T; ++lt)
+                for (int v = 0; v < 3; ++v) {
+                    const D3 x = tri_vertex(d, lt, v);
+                    const double h = E.vp[0] * x.x + E.vp[1] * x.y + E.vp[2] * x.z - E.cvp;
+                    // + f64 rounding of h and of the sampled points (convex
+                    // combinations rounded): far below 1e-9
+                    const double e = 1e-9 * (1.0 + fabs(x.x) + fabs(x.y) + fabs(x.z) + fabs(E.cvp));
+                    hmin = std::min(hmin, h - e);
+                    hmax = std::max(hmax, h + e);
+                }
+        }
+        if (!(hmin <= hmax)) continue;
+        const double eh = (double)U.eh;
+        if (hmin > m1) lc[0] = f32_upb(hmax / 2 + m2 + eh);
+        else if (hmax < -m1) lc[1] = f32_down(hmin / 2 - m2 - eh);
+    }
 }
 
 // The 64-B form of the BVH units (UnitC, pt_core.h), when every unit is a
@@ -745,6 +794,7 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         acc += d->tri_area[t];
         H->light_cum.push_back(acc);
     }
+    light_cull(H, d);
     SceneK& K = H->k;
     K.n_tri = T;
     K.n_obj_tri = d->n_obj_tri;
@@ -783,6 +833,7 @@ inline void bind_host(HostScene* H) {
     H->k.mat = H->mat.data();
     H->k.light_tri = H->light_tri.data();
     H->k.light_cum = H->light_cum.data();
+    H->k.unit_lc = H->unit_lc.data();
 }
 
 // first band row >= row_begin with iy % step == phase, and the band's row count
