@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 3
+#define PT_API_VERSION 4
 
 /* error codes */
 #define PT_OK 0
@@ -57,6 +57,9 @@ extern "C" {
                                           (counting kernels; synchronous)  */
 #define PT_FLAG_KERNEL_TIMES (1u << 6) /* wavefront renders: per-kernel HIP-event
                                           times into pt_stats (synchronous) */
+#define PT_FLAG_TREE_WALK (1u << 7)    /* wavefront renders: walk the shadow rays
+                                          through the BVH even when the scene
+                                          has a grid (same result)         */
 
 /*
  * Flattened scene, as produced by scene_reader.Scene

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pt_capi.h (structs, flags, error codes)."""
 import ctypes as C
 
-PT_API_VERSION = 3
+PT_API_VERSION = 4
 
 PT_OK = 0
 PT_EINVAL = -1
@@ -16,6 +16,7 @@ PT_FLAG_OUT_F64 = 1 << 3
 PT_FLAG_MEGAKERNEL = 1 << 4
 PT_FLAG_WALK_COUNT = 1 << 5
 PT_FLAG_KERNEL_TIMES = 1 << 6
+PT_FLAG_TREE_WALK = 1 << 7
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)

@@ -205,6 +205,14 @@ struct SceneK {
                                  // coplanar pair or degenerate: the walks read bunit)
     float bvh_eh, bvh_eq, bvh_qhi;   // maxima over bunit
     int32_t bvh_obj1;            // the BVH's one object, or -1 (several: from tri_obj)
+    // Uniform grid over the BVH units (pt_prepare.h build_grid; null gcell: no
+    // grid): cell (ix, iy, iz) = [g_org + (ix, iy, iz) h, + h) in the BVH's
+    // frame, its units gref[gcell[c] .. gcell[c + 1]) with c = (iz g_n[1] + iy)
+    // g_n[0] + ix.  The one-ray shadow walks march it (k_wf_shadow_grid).
+    const int32_t* gcell;        // [g_n[0] g_n[1] g_n[2] + 1] CSR starts into gref
+    const int32_t* gref;         // BVH unit indices (bunit / bunitc) per cell
+    float g_org[3], g_h;
+    int32_t g_n[3], n_gref;
     const float* unit_lc;        // [2 n_obj_unit] light-side cull thresholds of `unit`
                                  // (pt_prepare.h light_cull): a shadow ray from an origin
                                  // whose f32 plane value h has h > lc[0] or h < lc[1]

@@ -549,6 +549,68 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
     flush_walk_counts<COUNT>(c_q, c_nodes, c_units, wc);
 }
 
+// The shadow walks through the uniform grid (pt_path.h "grid shadow walks",
+// pt_prepare.h build_grid): one ray per work-item, persistent as k_wf_shadow.
+// A turn tests one unit of the lane's current cell (moving on through
+// emptied cells first), so the lanes of a wave stay busy whatever their
+// cells hold.  COUNT: cells entered as node visits, unit tests as leaf units.
+template <bool UC, bool COUNT>
+__global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow_grid(SceneK S, WfPath* __restrict__ W,
+                                                        WfShadowQ* __restrict__ SQ,
+                                                        const int32_t* __restrict__ list, int32_t* counters,
+                                                        unsigned long long* wc) {
+    uint32_t c_q = 0, c_cells = 0, c_units = 0;
+    const int32_t count = counters[0];
+    int32_t cb = 0, ce = 0;   // this wave's claimed list positions (wf_fetch)
+    int32_t slot = -1;
+    bool exhausted = false;
+    Shadow1 r;
+    F3 o32, inv;
+    int ogrp = -1;
+    GridTrav G;
+    G.live = false;
+    while (true) {
+        const bool need = slot < 0 && !exhausted;
+        if (__any(need)) {
+            const int32_t i = wf_fetch(need, &counters[1], cb, ce);
+            if (need) {
+                if (i < count) {
+                    const int32_t e = list[i];
+                    slot = e >> 2;
+                    if (COUNT) ++c_q;
+                    wf_get_shadow1(SQ[slot], e & 3, &o32, &ogrp, &r);
+                    inv = rcp_dir(r.d32);
+                    g_init(G, S, o32, r.d32, inv, r.hhi, shadow1_open(S, r));
+                    if (COUNT && G.live) ++c_cells;
+                } else {
+                    exhausted = true;
+                }
+            }
+        }
+        if (__all(slot < 0)) break;
+        if (slot >= 0) {
+            while (G.live && G.cur >= G.end) {   // on to a cell with units left
+                G.live = g_next(G, S, o32, inv);
+                if (COUNT && G.live) ++c_cells;
+            }
+            if (G.live) {
+                const int u = S.gref[G.cur++];
+                if (!g_mailbox(G, u)) {
+                    if (COUNT) ++c_units;
+                    const Spill sp{W[slot].sp, 1};
+                    shadow1_unit(S, bvh_unit<UC>(S, u), o32, ogrp, &r, sp);
+                    if (!shadow1_open(S, r)) G.live = false;
+                }
+            }
+            if (!G.live) {
+                wf_put_shadow1(&SQ[slot], r);
+                slot = -1;
+            }
+        }
+    }
+    flush_walk_counts<COUNT>(c_q, c_cells, c_units, wc);
+}
+
 template <bool UC, bool COUNT>
 __global__ __launch_bounds__(256, PT_CLOSEST_WAVES) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
                                                     WfClosestQ* __restrict__ CQ,
@@ -843,7 +905,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         if (prop.multiProcessorCount > 0) s->n_cu = prop.multiProcessorCount;
     }
     HostScene& H = s->host;
-    constexpr int kArrays = 15;
+    constexpr int kArrays = 17;
     const size_t sz[kArrays] = {H.unit.size() * sizeof(UnitF), H.trid.size() * sizeof(TriD),
                                 H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
                                 H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
@@ -852,11 +914,13 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
                                 H.bnode.size() * sizeof(BNode), H.bunit.size() * sizeof(UnitF),
                                 H.cnode.size() * sizeof(CNode), H.qnode.size() * sizeof(QNode),
                                 H.bunitc.size() * sizeof(UnitC), H.unit_eye.size() * sizeof(UnitF),
-                                H.unit_lc.size() * sizeof(float)};
+                                H.unit_lc.size() * sizeof(float), H.gcell.size() * sizeof(int32_t),
+                                H.gref.size() * sizeof(int32_t)};
     const void* src[kArrays] = {H.unit.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
                                 H.mat.data(), H.light_tri.data(), H.light_cum.data(),
                                 H.tri_grp.data(), H.bnode.data(), H.bunit.data(), H.cnode.data(),
-                                H.qnode.data(), H.bunitc.data(), H.unit_eye.data(), H.unit_lc.data()};
+                                H.qnode.data(), H.bunitc.data(), H.unit_eye.data(), H.unit_lc.data(),
+                                H.gcell.data(), H.gref.data()};
     size_t off[kArrays], total = 0;
     for (int i = 0; i < kArrays; ++i) { off[i] = total; total += align_up(sz[i]); }
     int rc = PT_OK;
@@ -886,6 +950,8 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     s->dev.bunitc = H.bunitc.empty() ? nullptr : (const UnitC*)(b + off[12]);
     s->dev.unit_eye = (const UnitF*)(b + off[13]);
     s->dev.unit_lc = (const float*)(b + off[14]);
+    s->dev.gcell = H.gcell.empty() ? nullptr : (const int32_t*)(b + off[15]);
+    s->dev.gref = H.gref.empty() ? nullptr : (const int32_t*)(b + off[16]);
     s->xb_surf = box_bound(H, false);
     s->xb_all = box_bound(H, true);
     *out = s;
@@ -1070,9 +1136,18 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
             else hipLaunchKernelGGL((k_wf_closest<false, false>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, q, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd, ws);
         }
     };
+    const bool use_grid = s->dev.gcell && !(flags & PT_FLAG_TREE_WALK);
     auto shadow_walk = [&](hipStream_t on) {
         const int32_t* l = lists;
-        if (s->dev.bunitc) {
+        if (use_grid) {
+            if (s->dev.bunitc) {
+                if (wcount) hipLaunchKernelGGL((k_wf_shadow_grid<true, true>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, wc);
+                else hipLaunchKernelGGL((k_wf_shadow_grid<true, false>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, wc);
+            } else {
+                if (wcount) hipLaunchKernelGGL((k_wf_shadow_grid<false, true>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, wc);
+                else hipLaunchKernelGGL((k_wf_shadow_grid<false, false>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, wc);
+            }
+        } else if (s->dev.bunitc) {
             if (wcount) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc, ovf_s);
             else hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc, ovf_s);
         } else {

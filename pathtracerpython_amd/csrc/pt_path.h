@@ -1548,6 +1548,82 @@ PT_HD void s1_units(const ShadowTrav1& T, const SceneK& S, Shadow1* r, const Spi
         shadow1_unit(S, bvh_unit<UC>(S, u0 + i), T.o32, T.ogrp, r, sp);
 }
 
+// ------------------------------------------------- grid shadow walks --
+// One shadow ray marched through the uniform grid over the BVH units
+// (pt_prepare.h build_grid: exactness argument there), cell by cell along
+// t in [-R, R] (two-sided, main.py:42-47), testing each cell's units with the
+// tree walk's leaf test (shadow1_unit).  A unit listed in several cells is
+// tested once per cell: any-hit results do not change (ray 2 keeps its lowest
+// occluding object).
+struct GridTrav {
+    int c[3];      // current cell
+    float tn[3];   // line parameter where the line leaves the cell, per axis
+    float tend;    // end of the clipped segment
+    int cur, end;  // the current cell's units: gref[cur .. end)
+    int last0, last1;   // the last two units tested (a unit spans a few cells)
+    bool live;
+};
+// true when unit u was one of the last two tested (its test would repeat);
+// else records it
+PT_HD bool g_mailbox(GridTrav& G, int u) {
+    if (u == G.last0 || u == G.last1) return true;
+    G.last1 = G.last0;
+    G.last0 = u;
+    return false;
+}
+PT_HD float g_cross(const SceneK& S, int a, int ci, float o, float inv) {
+    // the cell boundary the line crosses next on axis a (upper when inv > 0)
+    const float b = fmaf((float)(inv > 0.0f ? ci + 1 : ci), S.g_h, S.g_org[a]);
+    return (b - o) * inv;
+}
+PT_HD void g_load(GridTrav& G, const SceneK& S) {
+    const int c = (G.c[2] * S.g_n[1] + G.c[1]) * S.g_n[0] + G.c[0];
+    G.cur = S.gcell[c];
+    G.end = S.gcell[c + 1];
+}
+PT_HD void g_init(GridTrav& G, const SceneK& S, F3 o, F3 d, F3 inv, float R, bool open) {
+    const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, ii[3] = {inv.x, inv.y, inv.z};
+    float ta = -R, tb = R;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {   // clip the segment to the grid box
+        const float g1 = fmaf((float)S.g_n[a], S.g_h, S.g_org[a]);
+        const float t0 = (S.g_org[a] - oo[a]) * ii[a], t1 = (g1 - oo[a]) * ii[a];
+        ta = fmaxf(ta, fminf(t0, t1));
+        tb = fminf(tb, fmaxf(t0, t1));
+    }
+    G.live = open && ta <= tb;
+    G.tend = tb;
+    G.cur = G.end = 0;
+    G.last0 = G.last1 = -1;
+    const float ih = 1.0f / S.g_h;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float p = fmaf(ta, dd[a], oo[a]);
+        int ci = (int)floorf((p - S.g_org[a]) * ih);
+        ci = ci < 0 ? 0 : (ci >= S.g_n[a] ? S.g_n[a] - 1 : ci);
+        G.c[a] = ci;
+        G.tn[a] = g_cross(S, a, ci, oo[a], ii[a]);
+    }
+    if (G.live) g_load(G, S);
+}
+// to the next cell along the line; false past the segment's end or the grid
+PT_HD bool g_next(GridTrav& G, const SceneK& S, F3 o, F3 inv) {
+    const int a = (G.tn[0] <= G.tn[1]) ? (G.tn[0] <= G.tn[2] ? 0 : 2) : (G.tn[1] <= G.tn[2] ? 1 : 2);
+    const float ia = a == 0 ? inv.x : (a == 1 ? inv.y : inv.z);
+    const float oa = a == 0 ? o.x : (a == 1 ? o.y : o.z);
+    const float t = a == 0 ? G.tn[0] : (a == 1 ? G.tn[1] : G.tn[2]);
+    if (!(t <= G.tend)) return false;
+    int ci = (a == 0 ? G.c[0] : (a == 1 ? G.c[1] : G.c[2])) + (ia > 0.0f ? 1 : -1);
+    const int na = a == 0 ? S.g_n[0] : (a == 1 ? S.g_n[1] : S.g_n[2]);
+    if (ci < 0 || ci >= na) return false;
+    const float tn = g_cross(S, a, ci, oa, ia);
+    if (a == 0) { G.c[0] = ci; G.tn[0] = tn; }
+    else if (a == 1) { G.c[1] = ci; G.tn[1] = tn; }
+    else { G.c[2] = ci; G.tn[2] = tn; }
+    g_load(G, S);
+    return true;
+}
+
 // Standalone query (primary rays, the batched intersect_objects API).  d need
 // not be normalised (utils.py:110).  ogrp: coplanar group of the triangle the
 // origin lies on (-1: none).

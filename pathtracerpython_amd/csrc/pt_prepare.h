@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -32,6 +33,8 @@ struct HostScene {
     std::vector<int32_t> light_tri;
     std::vector<double> light_cum;
     std::vector<float> unit_lc;   // [2 n_obj_unit] light_cull thresholds
+    std::vector<int32_t> gcell;   // grid CSR starts (build_grid), empty: no grid
+    std::vector<int32_t> gref;
     SceneK k{};   // pointers unset; constants filled
 };
 
@@ -354,6 +357,133 @@ inline float f32_up(double x) {   // round to f32, never below x (x >= 0)
     float f = (float)x;
     if ((double)f < x) f = nextafterf(f, INFINITY);
     return f;
+}
+
+// Uniform grid over the BVH units for the one-ray shadow walks
+// (k_wf_shadow_grid, pt_path.h "grid walks").  A shadow ray is a line segment
+// |t| <= R (main.py:42-47, two-sided); a grid marches it cell by cell and tests
+// each cell's units, which for a mesh of many small triangles spread through a
+// volume (K5) costs far fewer instructions than a tree walk.  Exactness: a unit
+// is listed in every cell its box, inflated by delta = 128 u X, overlaps.  The
+// march follows the f32 line (centred origin, f32 direction: within ~20 u X of
+// the exact line for |t| <= 2 sqrt(3) X, as for the BVH's slab tests) and at
+// parameter t sits in a cell that the f32 line occupies up to the rounding of
+// the boundary crossings (a few u X), so every point where the reference's
+// line meets a unit is within delta of a visited cell's part of the line: the
+// unit is listed there.  Units are tested with the same verdicts as the tree
+// walk's leaves, each result decided the same way whatever the order (any
+// occluder closes rays 0 and 1; ray 2 keeps its lowest occluding object), so the
+// framebuffer is bit for bit the tree walk's.  Cell size: about
+// PT_GRID_DENSITY units per cell; no grid when the mesh packs too many units
+// into one cell (a grid pays for itself on volumes of small triangles).
+//
+// Measured (round 3, K5 at 1024^2 x 256 spp): bit for bit the
+// tree walk's frame, but the shadow walks take 2029-2947 ms per render
+// against the tree's 603 (densities 0.125-2 units per cell: 23-58 cells and
+// 23-91 unit tests per ray, each cell and each unit one dependent load, vs
+// ~55 dependent node / leaf loads per ray in the tree).  So the library does
+// not build it (PT_GRID 0); the host check build (tests/hostcheck) does and
+// checks the grid walk against the tree walk bit for bit.
+#ifndef PT_GRID
+#define PT_GRID 0
+#endif
+#ifndef PT_GRID_DENSITY
+#define PT_GRID_DENSITY 0.5
+#endif
+#ifndef PT_GRID_MAX_CELL
+#define PT_GRID_MAX_CELL 64
+#endif
+inline void build_grid(HostScene* H, const pt_scene_desc* d, double X) {
+    SceneK& K = H->k;
+    H->gcell.clear();
+    H->gref.clear();
+    K.g_org[0] = K.g_org[1] = K.g_org[2] = 0.f;
+    K.g_h = 0.f;
+    K.g_n[0] = K.g_n[1] = K.g_n[2] = 0;
+    K.n_gref = 0;
+    const int N = (int)H->bunit.size();
+    if (!PT_GRID || N == 0) return;
+    const double u = 1.0 / 16777216.0, delta = 128.0 * u * X;
+    const D3 C = d3(K.center[0], K.center[1], K.center[2]);
+    std::vector<double> box(6 * (size_t)N);
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = 0; i < N; ++i) {
+        const UnitF& U = H->bunit[i];
+        double* b = &box[6 * (size_t)i];
+        for (int a = 0; a < 3; ++a) { b[a] = INFINITY; b[3 + a] = -INFINITY; }
+        for (int m = 0; m < U.count; ++m)
+            for (int v = 0; v < 3; ++v) {
+                const D3 x = tri_vertex(d, U.t[m], v) - C;
+                const double xa[3] = {x.x, x.y, x.z};
+                for (int a = 0; a < 3; ++a) {
+                    b[a] = std::min(b[a], xa[a] - delta);
+                    b[3 + a] = std::max(b[3 + a], xa[a] + delta);
+                }
+            }
+        for (int a = 0; a < 3; ++a) {
+            if (!(b[a] <= b[3 + a]) || !std::isfinite(b[a]) || !std::isfinite(b[3 + a])) return;
+            lo[a] = std::min(lo[a], b[a]);
+            hi[a] = std::max(hi[a], b[3 + a]);
+        }
+    }
+    double vol = 1.0;
+    for (int a = 0; a < 3; ++a) vol *= std::max(hi[a] - lo[a], 1e-6 * X + 1e-30);
+    double h = std::cbrt(vol * PT_GRID_DENSITY / N);
+    int n[3];
+    float G0[3], hf = 0.f;
+    for (int tries = 0;; ++tries) {
+        if (tries > 64) return;
+        hf = f32_upb(h);
+        double cells = 1.0;
+        for (int a = 0; a < 3; ++a) {
+            G0[a] = f32_down(lo[a]);
+            n[a] = std::max(1, (int)std::ceil((hi[a] - (double)G0[a]) / (double)hf));
+            while ((double)G0[a] + (double)n[a] * (double)hf < hi[a]) ++n[a];
+            cells *= n[a];
+        }
+        if (n[0] <= 1024 && n[1] <= 1024 && n[2] <= 1024 && cells <= (double)(1 << 24)) break;
+        h *= 1.25;
+    }
+    const int64_t nc = (int64_t)n[0] * n[1] * n[2];
+    std::vector<int32_t> cnt(nc + 1, 0);
+    auto range = [&](const double* b, int a, int* i0, int* i1) {
+        *i0 = std::min(std::max((int)std::floor((b[a] - (double)G0[a]) / (double)hf), 0), n[a] - 1);
+        *i1 = std::min(std::max((int)std::floor((b[3 + a] - (double)G0[a]) / (double)hf), 0), n[a] - 1);
+    };
+    int64_t total = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int i = 0; i < N; ++i) {
+            const double* b = &box[6 * (size_t)i];
+            int x0, x1, y0, y1, z0, z1;
+            range(b, 0, &x0, &x1);
+            range(b, 1, &y0, &y1);
+            range(b, 2, &z0, &z1);
+            for (int z = z0; z <= z1; ++z)
+                for (int y = y0; y <= y1; ++y)
+                    for (int x = x0; x <= x1; ++x) {
+                        const int64_t c = ((int64_t)z * n[1] + y) * n[0] + x;
+                        if (pass == 0) ++cnt[c + 1];
+                        else H->gref[cnt[c]++] = i;
+                    }
+        }
+        if (pass == 0) {
+            int maxc = 0;
+            for (int64_t c = 0; c < nc; ++c) {
+                maxc = std::max(maxc, cnt[c + 1]);
+                cnt[c + 1] += cnt[c];
+            }
+            total = cnt[nc];
+            if (maxc > PT_GRID_MAX_CELL || total >= ((int64_t)1 << 31) - 1) return;
+            H->gcell.assign(cnt.begin(), cnt.end());
+            H->gref.assign((size_t)total, 0);
+        }
+    }
+    for (int a = 0; a < 3; ++a) {
+        K.g_org[a] = G0[a];
+        K.g_n[a] = n[a];
+    }
+    K.g_h = hf;
+    K.n_gref = (int32_t)total;
 }
 
 // Light-side cull of the uniform units' shadow tests (render loop,
@@ -814,6 +944,7 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     if (H->bunit.size() >= (size_t(1) << 24)) return "mesh too large: at most 2^24 BVH units";
     build_bvh(H, X);   // needs K.center and K.n_tri
     build_unitc(H);
+    build_grid(H, d, X);
     return "";
 }
 
@@ -834,6 +965,8 @@ inline void bind_host(HostScene* H) {
     H->k.light_tri = H->light_tri.data();
     H->k.light_cum = H->light_cum.data();
     H->k.unit_lc = H->unit_lc.data();
+    H->k.gcell = H->gcell.empty() ? nullptr : H->gcell.data();
+    H->k.gref = H->gref.empty() ? nullptr : H->gref.data();
 }
 
 // first band row >= row_begin with iy % step == phase, and the band's row count

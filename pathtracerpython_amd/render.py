@@ -18,6 +18,7 @@ import numpy as np
 
 from . import _native
 from ._abi import (PT_FLAG_COUNT, PT_FLAG_FORCE_F64, PT_FLAG_KERNEL_TIMES, PT_FLAG_MEGAKERNEL,
+                   PT_FLAG_TREE_WALK,
                    PT_FLAG_OUT_F64, PT_FLAG_RR, PT_FLAG_WALK_COUNT, PtStats, band_rows, make_params)
 from .pack import pack_scene
 
@@ -47,11 +48,13 @@ class Renderer:
     def params(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
                rr_depth=3, force_f64=False, count=False, out_f64=False, row_begin=0,
                row_end=None, row_step=1, row_phase=0, sample_begin=0, megakernel=False,
-               walk_count=False, kernel_times=False):
+               walk_count=False, kernel_times=False, tree_walk=False):
         """megakernel=True: scenes with a BVH render with the single kernel
         instead of the wavefront kernels (the same framebuffer, bit for bit).
         walk_count / kernel_times (wavefront renders): the walks' work counts /
-        per-kernel HIP-event times in the stats."""
+        per-kernel HIP-event times in the stats.  tree_walk=True: the
+        wavefront shadow walks go through the BVH even when the scene has a
+        grid (the same framebuffer, bit for bit)."""
         width = int(self.scene.width if width is None else width)
         height = int(self.scene.height if height is None else height)
         seed = self.scene.seed if seed is None else seed
@@ -59,7 +62,8 @@ class Renderer:
         flags = (PT_FLAG_RR if rr else 0) | (PT_FLAG_FORCE_F64 if force_f64 else 0) | \
             (PT_FLAG_COUNT if count else 0) | (PT_FLAG_OUT_F64 if out_f64 else 0) | \
             (PT_FLAG_MEGAKERNEL if megakernel else 0) | \
-            (PT_FLAG_WALK_COUNT if walk_count else 0) | (PT_FLAG_KERNEL_TIMES if kernel_times else 0)
+            (PT_FLAG_WALK_COUNT if walk_count else 0) | (PT_FLAG_KERNEL_TIMES if kernel_times else 0) | \
+            (PT_FLAG_TREE_WALK if tree_walk else 0)
         return make_params(width, height, spp, bounces, seed, flags, rr_depth, row_begin,
                            row_end, row_step, row_phase, sample_begin)
 

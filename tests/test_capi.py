@@ -45,7 +45,7 @@ def test_abi_struct_layout(hostcheck):
 
 def test_api_version():
     from pathtracerpython_amd._abi import PT_API_VERSION
-    assert _native.lib().pt_api_version() == PT_API_VERSION == 3
+    assert _native.lib().pt_api_version() == PT_API_VERSION == 4
 
 
 @pytest.mark.parametrize("H,step,phase,b,e", [(10, 1, 0, 0, 10), (10, 3, 1, 0, 10),
