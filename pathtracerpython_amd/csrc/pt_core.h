@@ -211,6 +211,7 @@ struct SceneK {
     // g_n[0] + ix.  The one-ray shadow walks march it (k_wf_shadow_grid).
     const int32_t* gcell;        // [g_n[0] g_n[1] g_n[2] + 1] CSR starts into gref
     const int32_t* gref;         // BVH unit indices (bunit / bunitc) per cell
+    const UnitC* gunitc;         // [n_gref] their 64-B records in cell order (PT_GRID_DUP)
     float g_org[3], g_h;
     int32_t g_n[3], n_gref;
     const float* unit_lc;        // [2 n_obj_unit] light-side cull thresholds of `unit`

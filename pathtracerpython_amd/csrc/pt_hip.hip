@@ -549,6 +549,12 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
     flush_walk_counts<COUNT>(c_q, c_nodes, c_units, wc);
 }
 
+#ifndef PT_GRID_FLAT
+#define PT_GRID_FLAT 1
+#endif
+#ifndef PT_GRID_DUP   // experiment: records duplicated in cell order (gunitc), prefetched
+#define PT_GRID_DUP 0
+#endif
 // The shadow walks through the uniform grid (pt_path.h "grid shadow walks",
 // pt_prepare.h build_grid): one ray per work-item, persistent as k_wf_shadow.
 // A turn tests one unit of the lane's current cell (moving on through
@@ -569,6 +575,9 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow_grid(SceneK 
     int ogrp = -1;
     GridTrav G;
     G.live = false;
+#if PT_GRID_DUP
+    UnitC pre{};
+#endif
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
@@ -582,6 +591,9 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow_grid(SceneK 
                     inv = rcp_dir(r.d32);
                     g_init(G, S, o32, r.d32, inv, r.hhi, shadow1_open(S, r));
                     if (COUNT && G.live) ++c_cells;
+#if PT_GRID_DUP
+                    if (G.live && G.cur < G.end) pre = S.gunitc[G.cur];
+#endif
                 } else {
                     exhausted = true;
                 }
@@ -589,11 +601,47 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow_grid(SceneK 
         }
         if (__all(slot < 0)) break;
         if (slot >= 0) {
+#if PT_GRID_DUP
+            // the cell's records in cell order, the next one loaded while
+            // this one is tested (UC scenes only: gunitc)
+            if (G.live && G.cur >= G.end) {
+                G.live = g_next(G, S, o32, inv);
+                if (COUNT && G.live) ++c_cells;
+                if (G.live && G.cur < G.end) pre = S.gunitc[G.cur];
+            } else if (G.live) {
+                const UnitC rec = pre;
+                ++G.cur;
+                if (G.cur < G.end) pre = S.gunitc[G.cur];
+                if (!g_mailbox(G, rec.t)) {
+                    if (COUNT) ++c_units;
+                    const Spill sp{W[slot].sp, 1};
+                    shadow1_unit(S, unitc_f(S, rec), o32, ogrp, &r, sp);
+                    if (!shadow1_open(S, r)) G.live = false;
+                }
+            }
+            if (!G.live) {
+                wf_put_shadow1(&SQ[slot], r);
+                slot = -1;
+            }
+        }
+    }
+    flush_walk_counts<COUNT>(c_q, c_cells, c_units, wc);
+}
+#else
+#if PT_GRID_FLAT
+            // a turn either moves on one cell or tests one unit (no wave-wide
+            // wait for the lane with the most empty cells in a row)
+            if (G.live && G.cur >= G.end) {
+                G.live = g_next(G, S, o32, inv);
+                if (COUNT && G.live) ++c_cells;
+            } else if (G.live) {
+#else
             while (G.live && G.cur >= G.end) {   // on to a cell with units left
                 G.live = g_next(G, S, o32, inv);
                 if (COUNT && G.live) ++c_cells;
             }
             if (G.live) {
+#endif
                 const int u = S.gref[G.cur++];
                 if (!g_mailbox(G, u)) {
                     if (COUNT) ++c_units;
@@ -610,6 +658,7 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow_grid(SceneK 
     }
     flush_walk_counts<COUNT>(c_q, c_cells, c_units, wc);
 }
+#endif
 
 template <bool UC, bool COUNT>
 __global__ __launch_bounds__(256, PT_CLOSEST_WAVES) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
@@ -905,7 +954,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         if (prop.multiProcessorCount > 0) s->n_cu = prop.multiProcessorCount;
     }
     HostScene& H = s->host;
-    constexpr int kArrays = 17;
+    constexpr int kArrays = 18;
     const size_t sz[kArrays] = {H.unit.size() * sizeof(UnitF), H.trid.size() * sizeof(TriD),
                                 H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
                                 H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
@@ -915,12 +964,12 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
                                 H.cnode.size() * sizeof(CNode), H.qnode.size() * sizeof(QNode),
                                 H.bunitc.size() * sizeof(UnitC), H.unit_eye.size() * sizeof(UnitF),
                                 H.unit_lc.size() * sizeof(float), H.gcell.size() * sizeof(int32_t),
-                                H.gref.size() * sizeof(int32_t)};
+                                H.gref.size() * sizeof(int32_t), H.gunitc.size() * sizeof(UnitC)};
     const void* src[kArrays] = {H.unit.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
                                 H.mat.data(), H.light_tri.data(), H.light_cum.data(),
                                 H.tri_grp.data(), H.bnode.data(), H.bunit.data(), H.cnode.data(),
                                 H.qnode.data(), H.bunitc.data(), H.unit_eye.data(), H.unit_lc.data(),
-                                H.gcell.data(), H.gref.data()};
+                                H.gcell.data(), H.gref.data(), H.gunitc.data()};
     size_t off[kArrays], total = 0;
     for (int i = 0; i < kArrays; ++i) { off[i] = total; total += align_up(sz[i]); }
     int rc = PT_OK;
@@ -952,6 +1001,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     s->dev.unit_lc = (const float*)(b + off[14]);
     s->dev.gcell = H.gcell.empty() ? nullptr : (const int32_t*)(b + off[15]);
     s->dev.gref = H.gref.empty() ? nullptr : (const int32_t*)(b + off[16]);
+    s->dev.gunitc = H.gunitc.empty() ? nullptr : (const UnitC*)(b + off[17]);
     s->xb_surf = box_bound(H, false);
     s->xb_all = box_bound(H, true);
     *out = s;
@@ -1136,7 +1186,7 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
             else hipLaunchKernelGGL((k_wf_closest<false, false>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, q, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd, ws);
         }
     };
-    const bool use_grid = s->dev.gcell && !(flags & PT_FLAG_TREE_WALK);
+    const bool use_grid = s->dev.gcell && (!PT_GRID_DUP || s->dev.gunitc) && !(flags & PT_FLAG_TREE_WALK);
     auto shadow_walk = [&](hipStream_t on) {
         const int32_t* l = lists;
         if (use_grid) {

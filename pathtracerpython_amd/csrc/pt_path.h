@@ -963,10 +963,7 @@ PT_HD void ctrav_node(ClosestTrav& T, const ClosestStack& K, const SceneK& S, co
 // the units of leaf `ref` (<= -2: leaf codes have a unit count >= 1)
 // BVH unit i as the walks test it: UC = from the 64-B form (the caller
 // checked S.bunitc; a compile-time choice, so only one record is loaded)
-template <bool UC>
-PT_HD UnitF bvh_unit(const SceneK& S, int i) {
-    if (!UC) return S.bunit[i];
-    const UnitC C = S.bunitc[i];
+PT_HD UnitF unitc_f(const SceneK& S, const UnitC& C) {
     UnitF U;
     U.n[0] = C.n[0]; U.n[1] = C.n[1]; U.n[2] = C.n[2];
     U.cn = C.cn;
@@ -984,6 +981,11 @@ PT_HD UnitF bvh_unit(const SceneK& S, int i) {
     U.tri[0] = C.tri;
     U.tri[1] = TriB{};
     return U;
+}
+template <bool UC>
+PT_HD UnitF bvh_unit(const SceneK& S, int i) {
+    if (!UC) return S.bunit[i];
+    return unitc_f(S, S.bunitc[i]);
 }
 template <bool COUNT, bool UC = false>
 PT_HD void ctrav_units(const ClosestTrav& T, const SceneK& S, ClosestAcc* ca, const Spill& sp,

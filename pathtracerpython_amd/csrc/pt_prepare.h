@@ -35,6 +35,7 @@ struct HostScene {
     std::vector<float> unit_lc;   // [2 n_obj_unit] light_cull thresholds
     std::vector<int32_t> gcell;   // grid CSR starts (build_grid), empty: no grid
     std::vector<int32_t> gref;
+    std::vector<UnitC> gunitc;    // bunitc[gref[i]] (PT_GRID_DUP)
     SceneK k{};   // pointers unset; constants filled
 };
 
@@ -397,6 +398,7 @@ inline void build_grid(HostScene* H, const pt_scene_desc* d, double X) {
     SceneK& K = H->k;
     H->gcell.clear();
     H->gref.clear();
+    H->gunitc.clear();
     K.g_org[0] = K.g_org[1] = K.g_org[2] = 0.f;
     K.g_h = 0.f;
     K.g_n[0] = K.g_n[1] = K.g_n[2] = 0;
@@ -484,6 +486,10 @@ inline void build_grid(HostScene* H, const pt_scene_desc* d, double X) {
     }
     K.g_h = hf;
     K.n_gref = (int32_t)total;
+    if (!H->bunitc.empty()) {
+        H->gunitc.resize((size_t)total);
+        for (int64_t i = 0; i < total; ++i) H->gunitc[i] = H->bunitc[H->gref[i]];
+    }
 }
 
 // Light-side cull of the uniform units' shadow tests (render loop,
@@ -967,6 +973,7 @@ inline void bind_host(HostScene* H) {
     H->k.unit_lc = H->unit_lc.data();
     H->k.gcell = H->gcell.empty() ? nullptr : H->gcell.data();
     H->k.gref = H->gref.empty() ? nullptr : H->gref.data();
+    H->k.gunitc = H->gunitc.empty() ? nullptr : H->gunitc.data();
 }
 
 // first band row >= row_begin with iy % step == phase, and the band's row count
