@@ -555,6 +555,9 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
 #ifndef PT_GRID_DUP   // experiment: records duplicated in cell order (gunitc), prefetched
 #define PT_GRID_DUP 0
 #endif
+#ifndef PT_GRID_LA    // experiment (with PT_GRID_DUP): the next cell's range loaded a cell ahead
+#define PT_GRID_LA 0
+#endif
 // The shadow walks through the uniform grid (pt_path.h "grid shadow walks",
 // pt_prepare.h build_grid): one ray per work-item, persistent as k_wf_shadow.
 // A turn tests one unit of the lane's current cell (moving on through
@@ -578,6 +581,10 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow_grid(SceneK 
 #if PT_GRID_DUP
     UnitC pre{};
 #endif
+#if PT_GRID_DUP && PT_GRID_LA
+    bool nlive = false;
+    int ncur = 0, nend = 0;
+#endif
     while (true) {
         const bool need = slot < 0 && !exhausted;
         if (__any(need)) {
@@ -594,6 +601,14 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow_grid(SceneK 
 #if PT_GRID_DUP
                     if (G.live && G.cur < G.end) pre = S.gunitc[G.cur];
 #endif
+#if PT_GRID_DUP && PT_GRID_LA
+                    nlive = G.live && g_adv(G, S, o32, inv);
+                    if (nlive) {
+                        const int c = (G.c[2] * S.g_n[1] + G.c[1]) * S.g_n[0] + G.c[0];
+                        ncur = S.gcell[c];
+                        nend = S.gcell[c + 1];
+                    }
+#endif
                 } else {
                     exhausted = true;
                 }
@@ -602,6 +617,37 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow_grid(SceneK 
         if (__all(slot < 0)) break;
         if (slot >= 0) {
 #if PT_GRID_DUP
+#if PT_GRID_LA
+            // one cell of look-ahead: the DDA cursor G runs a cell ahead and
+            // that cell's range (ncur, nend) is loaded while the current
+            // cell's records are tested
+            if (G.live && G.cur >= G.end) {
+                if (!nlive) {
+                    G.live = false;
+                } else {
+                    G.cur = ncur;
+                    G.end = nend;
+                    if (COUNT) ++c_cells;
+                    if (G.cur < G.end) pre = S.gunitc[G.cur];
+                    nlive = g_adv(G, S, o32, inv);
+                    if (nlive) {
+                        const int c = (G.c[2] * S.g_n[1] + G.c[1]) * S.g_n[0] + G.c[0];
+                        ncur = S.gcell[c];
+                        nend = S.gcell[c + 1];
+                    }
+                }
+            } else if (G.live) {
+                const UnitC rec = pre;
+                ++G.cur;
+                if (G.cur < G.end) pre = S.gunitc[G.cur];
+                if (!g_mailbox(G, rec.t)) {
+                    if (COUNT) ++c_units;
+                    const Spill sp{W[slot].sp, 1};
+                    shadow1_unit(S, unitc_f(S, rec), o32, ogrp, &r, sp);
+                    if (!shadow1_open(S, r)) G.live = false;
+                }
+            }
+#else
             // the cell's records in cell order, the next one loaded while
             // this one is tested (UC scenes only: gunitc)
             if (G.live && G.cur >= G.end) {
@@ -619,6 +665,7 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow_grid(SceneK 
                     if (!shadow1_open(S, r)) G.live = false;
                 }
             }
+#endif
             if (!G.live) {
                 wf_put_shadow1(&SQ[slot], r);
                 slot = -1;

@@ -1609,7 +1609,14 @@ PT_HD void g_init(GridTrav& G, const SceneK& S, F3 o, F3 d, F3 inv, float R, boo
     if (G.live) g_load(G, S);
 }
 // to the next cell along the line; false past the segment's end or the grid
+PT_HD bool g_adv(GridTrav& G, const SceneK& S, F3 o, F3 inv);
 PT_HD bool g_next(GridTrav& G, const SceneK& S, F3 o, F3 inv) {
+    if (!g_adv(G, S, o, inv)) return false;
+    g_load(G, S);
+    return true;
+}
+// the DDA step alone (no load of the new cell's range)
+PT_HD bool g_adv(GridTrav& G, const SceneK& S, F3 o, F3 inv) {
     const int a = (G.tn[0] <= G.tn[1]) ? (G.tn[0] <= G.tn[2] ? 0 : 2) : (G.tn[1] <= G.tn[2] ? 1 : 2);
     const float ia = a == 0 ? inv.x : (a == 1 ? inv.y : inv.z);
     const float oa = a == 0 ? o.x : (a == 1 ? o.y : o.z);
@@ -1622,7 +1629,6 @@ PT_HD bool g_next(GridTrav& G, const SceneK& S, F3 o, F3 inv) {
     if (a == 0) { G.c[0] = ci; G.tn[0] = tn; }
     else if (a == 1) { G.c[1] = ci; G.tn[1] = tn; }
     else { G.c[2] = ci; G.tn[2] = tn; }
-    g_load(G, S);
     return true;
 }
 
