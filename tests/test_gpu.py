@@ -330,6 +330,10 @@ def test_wavefront_k5_equals_single_kernel(k5small, W, spp, B, rr):
         # a band and a sample slice of the same image (kernel reuse, odd sizes)
         band = r.render(W, W, spp, B, 9, rr=rr, out_f64=True, row_begin=7, row_end=W - 3)
         assert np.array_equal(band, wf[3:W - 7])
+        # PT_FLAG_TREE_WALK: the shipped library builds no grid, so the
+        # shadow walks are the tree's either way (same frame)
+        tw = r.render_params(r.params(W, W, spp, B, 9, rr=rr, out_f64=True, tree_walk=True))
+        assert np.array_equal(tw, wf)
     rows = [0, W // 2, W - 1]
     pix = np.array([ix * W + iy for iy in rows for ix in range(0, W, 3)], dtype=np.int64)
     ref, _ = oracle.render(pk, W, W, spp, B, 9, flags=1 if rr else 0, pixels=pix)

@@ -270,6 +270,13 @@ def test_grid_shadow_walk_equals_tree_walk(hostcheck, tmp_path, kind):
     assert np.array_equal(outs[0], outs[1])
 
 
+def test_no_grid_without_mesh(hostcheck, cornell):
+    """Scenes without a BVH get no grid (build_grid runs on BVH units only)."""
+    info = (C.c_int32 * 5)()
+    assert hostcheck.hc_grid_info(C.byref(pack_scene(cornell).desc), info) == 0
+    assert list(info) == [0, 0, 0, 0, 0]
+
+
 def test_mesh_golden_bvh_and_wavefront(hostcheck, mesh_golden):
     """The host build's BVH walks (forced f64 and hybrid) and its wavefront
     state machine on the edge-case mesh scene, against the reference's render
