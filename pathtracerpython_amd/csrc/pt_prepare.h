@@ -496,9 +496,9 @@ inline void build_grid(HostScene* H, const pt_scene_desc* d, double X) {
 // pt_path.h).  A shadow ray from P toward a light point L is the line
 // P + s (L - P), |s| < 1 (main.py:37-47: two-sided, squared distance below
 // |L - P|^2).  Let h be a member triangle's signed plane distance (its
-// reference plane, utils.py:109-111).  If every light vertex has h > m1 (the
-// light strictly on the positive side: so has every sampled L, a convex
-// combination) and h(P) > max_L h / 2 + m2, the line meets the plane at
+// reference plane, utils.py:109-111).  If every corner of the light's box
+// has h > m1 (the light strictly on the positive side: so has every sampled
+// L, a point of the box) and h(P) > max h / 2 + m2, the line meets the plane at
 // s = h(P) / (h(P) - h(L)) with |s| - 1 >= min(m1 / h(P), 2 m2 / max h) > 0:
 // beyond L (h(L) < h(P)) or behind P farther than |L - P| (h(L) > h(P)),
 // certainly outside the reference's range for every light sample.  The
@@ -513,25 +513,34 @@ inline void light_cull(HostScene* H, const pt_scene_desc* d) {
     const int T = d->n_tri;
     const double m1 = 1e-6, m2 = 1e-6;
     H->unit_lc.assign(2 * (size_t)H->k.n_obj_unit, 0.f);
+    // the light's box: every sampled point lies in it (a convex combination
+    // of a light triangle's vertices), so h over its 8 corners bounds h over
+    // the light (cost independent of the light's triangle count)
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int lt = d->n_obj_tri; lt < T; ++lt)
+        for (int v = 0; v < 3; ++v) {
+            const D3 x = tri_vertex(d, lt, v);
+            const double xa[3] = {x.x, x.y, x.z};
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], xa[a]); hi[a] = std::max(hi[a], xa[a]); }
+        }
     for (int u = 0; u < H->k.n_obj_unit; ++u) {
         const UnitF& U = H->unit[u];
         float* lc = &H->unit_lc[2 * (size_t)u];
         lc[0] = INFINITY;
         lc[1] = -INFINITY;
-        if (!(U.eh >= 0.f) || !(U.eh < 1e30f) || d->n_obj_tri >= T) continue;   // degenerate / no light
+        if (!(U.eh >= 0.f) || !(U.eh < 1e30f) || !(lo[0] <= hi[0])) continue;   // degenerate / no light
         double hmin = INFINITY, hmax = -INFINITY;
         for (int m = 0; m < U.count; ++m) {
             const TriD& E = H->trid[U.t[m]];
-            for (int lt = d->n_obj_tri; lt < T; ++lt)
-                for (int v = 0; v < 3; ++v) {
-                    const D3 x = tri_vertex(d, lt, v);
-                    const double h = E.vp[0] * x.x + E.vp[1] * x.y + E.vp[2] * x.z - E.cvp;
-                    // + f64 rounding of h and of the sampled points (convex
-                    // combinations rounded): far below 1e-9
-                    const double e = 1e-9 * (1.0 + fabs(x.x) + fabs(x.y) + fabs(x.z) + fabs(E.cvp));
-                    hmin = std::min(hmin, h - e);
-                    hmax = std::max(hmax, h + e);
-                }
+            for (int c = 0; c < 8; ++c) {
+                const D3 x = d3((c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]);
+                const double h = E.vp[0] * x.x + E.vp[1] * x.y + E.vp[2] * x.z - E.cvp;
+                // + f64 rounding of h and of the sampled points (convex
+                // combinations rounded): far below 1e-9
+                const double e = 1e-9 * (1.0 + fabs(x.x) + fabs(x.y) + fabs(x.z) + fabs(E.cvp));
+                hmin = std::min(hmin, h - e);
+                hmax = std::max(hmax, h + e);
+            }
         }
         if (!(hmin <= hmax)) continue;
         const double eh = (double)U.eh;
