@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 4
+#define PT_API_VERSION 5
 
 /* error codes */
 #define PT_OK 0
@@ -40,6 +40,7 @@ extern "C" {
 #define PT_ENOMEM (-3)     /* device or host allocation failed */
 #define PT_ENODEV (-4)     /* no usable gfx950 device */
 #define PT_EUNSUPPORTED (-5) /* pt_obj_load: input outside the fast reader's subset */
+#define PT_ETIMEOUT (-6)   /* pt_wait_flags: the flags did not arrive in time */
 
 /* pt_render flags */
 #define PT_FLAG_RR (1u << 0)           /* Russian roulette (build extension) */
@@ -57,9 +58,9 @@ extern "C" {
                                           (counting kernels; synchronous)  */
 #define PT_FLAG_KERNEL_TIMES (1u << 6) /* wavefront renders: per-kernel HIP-event
                                           times into pt_stats (synchronous) */
-#define PT_FLAG_TREE_WALK (1u << 7)    /* wavefront renders: walk the shadow rays
-                                          through the BVH even when the scene
-                                          has a grid (same result)         */
+/* bit 7: reserved (v4's PT_FLAG_TREE_WALK, retired in v5 with the grid-walk
+   experiment it selected against; the library rejects it)                */
+#define PT_FLAG_RESERVED7 (1u << 7)
 
 /*
  * Flattened scene, as produced by scene_reader.Scene
@@ -88,9 +89,20 @@ typedef struct pt_scene_desc {
  * row_begin <= iy < row_end and iy % row_step == row_phase, which covers
  * contiguous bands (row_step 1) and the interleaved bands used for
  * multi-GPU balance.  Output: image orientation, float32 (float64 with
- * PT_FLAG_OUT_F64) out[(height-1-iy)][ix][3] restricted to the launched rows, packed in
- * launch order (see pt_band_rows).  Values are the averaged radiance before
- * make_image's min-max normalisation (main.py:274-280).                    */
+ * PT_FLAG_OUT_F64) out[(height-1-iy)][ix][3] restricted to the launched rows,
+ * in launch order (see pt_band_rows), one output row every out_row_stride
+ * elements (0: packed, width*3) — a band can be written straight into its
+ * rows of a whole frame (out = the frame's row of the band's top iy, stride =
+ * row_step*width*3).  Values are the averaged radiance before make_image's
+ * min-max normalisation (main.py:274-280).
+ *
+ * lanes_per_pixel: 0 lets the library choose the work-items per pixel of the
+ * launch (from the launch's size and the device: one rank's band of an N-GPU
+ * split gets more lanes per pixel than the whole frame); a power of two
+ * <= min(64, spp) fixes it.  A pixel's samples are summed in an order that
+ * follows its lane count, so two launches covering a pixel give bit-identical
+ * values when they use the same lanes_per_pixel, and values within ~1e-15
+ * relative of each other otherwise.                                        */
 typedef struct pt_render_params {
     int32_t width, height;
     int32_t spp;             /* main.py -r                                     */
@@ -100,7 +112,9 @@ typedef struct pt_render_params {
     int32_t rr_depth;        /* first bounce that may be terminated by RR     */
     int32_t row_begin, row_end, row_step, row_phase;
     int32_t sample_begin;    /* first sample index (spp-split renders)        */
-    int32_t reserved;
+    int32_t out_row_stride;  /* elements between output rows (0: width*3)     */
+    int32_t lanes_per_pixel; /* 0: chosen per launch; else fixed (see above)  */
+    int32_t reserved;        /* 0 */
 } pt_render_params;
 
 /* Work counters (PT_FLAG_COUNT); reference-semantics test counts are those
@@ -151,7 +165,8 @@ int pt_band_rows(const pt_render_params* p, int32_t* rows);
 int pt_render_device(pt_scene* scene, const pt_render_params* p,
                      void* out_rgb_dev, void* stream, pt_stats* stats);
 
-/* Same, synchronous, with a host output buffer (rows*width*3 elements). */
+/* Same, synchronous, with a host output buffer (rows*width*3 elements, or
+ * rows rows of out_row_stride elements). */
 int pt_render(pt_scene* scene, const pt_render_params* p, void* out_rgb_host,
               pt_stats* stats);
 
@@ -163,10 +178,15 @@ int pt_render(pt_scene* scene, const pt_render_params* p, void* out_rgb_host,
  * rows with (iy - row_begin) % n == i, all devices concurrently, and each
  * band is copied with one strided device-to-host copy straight into its rows
  * of out_rgb_host ((row_end-row_begin) x width x 3, the layout pt_render
- * writes for the whole range).  Bit-identical to pt_render of the same range
- * on one device.  Synchronous.  stats (optional) receives the per-device sums
- * of every field (PT_FLAG_COUNT / PT_FLAG_WALK_COUNT / PT_FLAG_KERNEL_TIMES
- * renders then run one device at a time). */
+ * writes for the whole range; p->out_row_stride must be 0).  Bit-identical to
+ * pt_render of the same range on one device when p->lanes_per_pixel is set
+ * (the same value for both); with 0 each band's launch chooses its own
+ * lanes per pixel and values agree to ~1e-15 relative (see
+ * pt_render_params).  Synchronous.  On an error the devices already launched
+ * are drained before it returns, so the handles and out_rgb_host are free
+ * for reuse.  stats (optional) receives the per-device sums of every field
+ * (PT_FLAG_COUNT / PT_FLAG_WALK_COUNT / PT_FLAG_KERNEL_TIMES renders then run
+ * one device at a time). */
 int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* p,
                     void* out_rgb_host, pt_stats* stats);
 
@@ -199,6 +219,31 @@ int pt_compute_color(pt_scene* scene, const int32_t* obj, const double* point,
 int pt_assemble_bands_device(const void* tiles_dev, int32_t world, int32_t max_rows,
                              int32_t width, int32_t height, uint32_t flags, void* out_dev,
                              void* stream);
+
+/* Host frames (the metric's framebuffer ends in host
+ * memory; §8(e): the N ranks' bands make one frame).  The reference collects
+ * the pool workers' colours into the parent's list through pipes
+ * (main.py:204, :224-231); here each GPU writes its band straight into its
+ * rows of one frame in page-locked host memory — shared by the rank
+ * processes of one node (e.g. a /dev/shm mapping) — through a band render
+ * with out = pt_host_map's device address of the band's first row and
+ * out_row_stride = row_step*width*3, so the framebuffer crosses PCIe while the
+ * kernel runs, each GPU over its own link.  Completion is a flag per rank in
+ * the same memory: pt_signal writes it on the render's stream after the
+ * render (system-scope release, so the band's stores are visible first), the
+ * consumer waits for all flags with pt_wait_flags.
+ *
+ * pt_host_map page-locks [host, host+bytes) (caller-owned, page-aligned, e.g.
+ * an mmap) for every device of the process and returns the address kernels
+ * use for it; pt_host_unmap releases it (after the work using it is done). */
+int pt_host_map(void* host, uint64_t bytes, void** dev_ptr);
+int pt_host_unmap(void* host);
+/* After all work queued on `stream` so far: *flag_dev = value (64-bit store,
+ * system scope, release).  flag_dev: a pt_host_map address or device memory. */
+int pt_signal(uint64_t* flag_dev, uint64_t value, void* stream);
+/* Host: spin until flags[i * stride] >= value for i < n (relaxed loads, then
+ * an acquire fence), or PT_ETIMEOUT after timeout_s seconds. */
+int pt_wait_flags(const uint64_t* flags, int32_t n, int32_t stride, uint64_t value, double timeout_s);
 
 /* Image finalisation of make_image (utils.py:150-161) on the device:
  * global min over the whole height x width x 3 array, shift, divide by the

@@ -1,13 +1,15 @@
 """ctypes mirror of include/pt_capi.h (structs, flags, error codes)."""
 import ctypes as C
 
-PT_API_VERSION = 4
+PT_API_VERSION = 5
 
 PT_OK = 0
 PT_EINVAL = -1
 PT_EHIP = -2
 PT_ENOMEM = -3
 PT_ENODEV = -4
+PT_EUNSUPPORTED = -5
+PT_ETIMEOUT = -6
 
 PT_FLAG_RR = 1 << 0
 PT_FLAG_FORCE_F64 = 1 << 1
@@ -16,7 +18,7 @@ PT_FLAG_OUT_F64 = 1 << 3
 PT_FLAG_MEGAKERNEL = 1 << 4
 PT_FLAG_WALK_COUNT = 1 << 5
 PT_FLAG_KERNEL_TIMES = 1 << 6
-PT_FLAG_TREE_WALK = 1 << 7
+# bit 7: reserved (v4's PT_FLAG_TREE_WALK, retired in v5)
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
@@ -40,6 +42,7 @@ class PtRenderParams(C.Structure):
         ("rr_depth", C.c_int32), ("row_begin", C.c_int32),
         ("row_end", C.c_int32), ("row_step", C.c_int32),
         ("row_phase", C.c_int32), ("sample_begin", C.c_int32),
+        ("out_row_stride", C.c_int32), ("lanes_per_pixel", C.c_int32),
         ("reserved", C.c_int32),
     ]
 
@@ -74,7 +77,7 @@ class PtStats(C.Structure):
 
 def make_params(width, height, spp, bounces, seed, flags=0, rr_depth=3,
                 row_begin=0, row_end=None, row_step=1, row_phase=0,
-                sample_begin=0):
+                sample_begin=0, out_row_stride=0, lanes_per_pixel=0):
     p = PtRenderParams()
     p.width, p.height, p.spp, p.bounces = int(width), int(height), int(spp), int(bounces)
     p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
@@ -85,7 +88,19 @@ def make_params(width, height, spp, bounces, seed, flags=0, rr_depth=3,
     p.row_step = int(row_step)
     p.row_phase = int(row_phase)
     p.sample_begin = int(sample_begin)
+    p.out_row_stride = int(out_row_stride)
+    p.lanes_per_pixel = int(lanes_per_pixel)
     return p
+
+
+def with_flags(p, add=0, **fields):
+    """A copy of params p with flag bits `add` set and any fields replaced."""
+    q = PtRenderParams()
+    C.pointer(q)[0] = p
+    q.flags = p.flags | int(add)
+    for k, v in fields.items():
+        setattr(q, k, int(v))
+    return q
 
 
 def band_rows(height, row_begin=0, row_end=None, row_step=1, row_phase=0):

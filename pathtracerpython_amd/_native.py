@@ -42,6 +42,10 @@ def _bind(lib):
         "pt_image_u8": ([vp, C.c_int32, C.c_int32, C.c_uint32, vp], C.c_int),
         "pt_assemble_bands_device": ([vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_uint32,
                                       vp, vp], C.c_int),
+        "pt_host_map": ([vp, C.c_uint64, C.POINTER(vp)], C.c_int),
+        "pt_host_unmap": ([vp], C.c_int),
+        "pt_signal": ([vp, C.c_uint64, vp], C.c_int),
+        "pt_wait_flags": ([vp, C.c_int32, C.c_int32, C.c_uint64, C.c_double], C.c_int),
         "pt_obj_load": ([C.c_char_p, C.POINTER(C.POINTER(PtMesh))], C.c_int),
         "pt_mesh_free": ([C.POINTER(PtMesh)], None),
     }
@@ -55,8 +59,8 @@ def _bind(lib):
 EXPORTS = ("pt_api_version", "pt_last_error", "pt_device_count", "pt_scene_create",
            "pt_scene_create_on", "pt_render_multi", "pt_scene_destroy", "pt_band_rows",
            "pt_render_device", "pt_render", "pt_last_kernel_ms", "pt_intersect_objects", "pt_compute_color",
-           "pt_image_u8_device", "pt_image_u8", "pt_assemble_bands_device", "pt_obj_load",
-           "pt_mesh_free")
+           "pt_image_u8_device", "pt_image_u8", "pt_assemble_bands_device", "pt_host_map",
+           "pt_host_unmap", "pt_signal", "pt_wait_flags", "pt_obj_load", "pt_mesh_free")
 
 
 def lib():

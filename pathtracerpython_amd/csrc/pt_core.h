@@ -205,19 +205,6 @@ struct SceneK {
                                  // coplanar pair or degenerate: the walks read bunit)
     float bvh_eh, bvh_eq, bvh_qhi;   // maxima over bunit
     int32_t bvh_obj1;            // the BVH's one object, or -1 (several: from tri_obj)
-    // Uniform grid over the BVH units (pt_prepare.h build_grid; null gcell: no
-    // grid): cell (ix, iy, iz) = [g_org + (ix, iy, iz) h, + h) in the BVH's
-    // frame, its units gref[gcell[c] .. gcell[c + 1]) with c = (iz g_n[1] + iy)
-    // g_n[0] + ix.  The one-ray shadow walks march it (k_wf_shadow_grid).
-    const int32_t* gcell;        // [g_n[0] g_n[1] g_n[2] + 1] CSR starts into gref
-    const int32_t* gref;         // BVH unit indices (bunit / bunitc) per cell
-    const UnitC* gunitc;         // [n_gref] their 64-B records in cell order (PT_GRID_DUP)
-    float g_org[3], g_h;
-    int32_t g_n[3], n_gref;
-    const float* unit_lc;        // [2 n_obj_unit] light-side cull thresholds of `unit`
-                                 // (pt_prepare.h light_cull): a shadow ray from an origin
-                                 // whose f32 plane value h has h > lc[0] or h < lc[1]
-                                 // certainly misses the unit, whichever light point it takes
 };
 
 // ------------------------------------------------------------------ RNG --
@@ -225,44 +212,9 @@ struct SceneK {
 // (pixel, sample, bounce, slot>>2); see tests/golden/philox_ref.py.
 // The 4 blocks of one (pixel, sample, bounce) — slots 0..15 — in lockstep:
 // four independent 10-round chains interleaved, instead of one chain at a time
-// Values a caller keeps across its bounce loop, made opaque to the optimiser
-// here (the seed is the same for every lane of a launch): the Philox round-0 products of the pixel and the key schedule are
-// then recomputed per call (a few integer ops) instead of being hoisted out
-// of the loop into registers it does not have (they went to scratch).
-PT_HD uint32_t pt_opaque(uint32_t v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+v"(v));
-#endif
-    return v;
-}
-PT_HD uint32_t pt_opaque_s(uint32_t v) {   // a wave-uniform value (kept in an SGPR)
-#if defined(__HIP_DEVICE_COMPILE__)
-    v = __builtin_amdgcn_readfirstlane(v);
-    asm volatile("" : "+s"(v));
-#endif
-    return v;
-}
-#ifndef PT_RNG_OPQ
-#define PT_RNG_OPQ 0
-#endif
 PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce,
                        uint32_t w[16]) {
-#ifdef PT_ABL_CHEAPRNG   // timing ablation only (a different stream)
-    uint32_t h = pixel * 0x9E3779B1u ^ sample * 0x85EBCA77u ^ bounce * 0xC2B2AE3Du ^ (uint32_t)seed;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h += 0x297A2D39u; w[i] = h;
-    }
-    return;
-#endif
-#if PT_RNG_OPQ & 1
-    pixel = pt_opaque(pixel);
-#endif
-#if PT_RNG_OPQ & 2
-    uint32_t k0 = pt_opaque_s((uint32_t)seed), k1 = pt_opaque_s((uint32_t)(seed >> 32));
-#else
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#endif
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
         w[4 * b] = pixel; w[4 * b + 1] = sample; w[4 * b + 2] = bounce; w[4 * b + 3] = (uint32_t)b;
@@ -288,14 +240,7 @@ PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t 
 // One Philox4x32-10 block: slots 4 blk .. 4 blk + 3 of (pixel, sample, bounce)
 PT_HD void rng_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t blk,
                      uint32_t c[4]) {
-#if PT_RNG_OPQ & 1
-    pixel = pt_opaque(pixel);
-#endif
-#if PT_RNG_OPQ & 2
-    uint32_t k0 = pt_opaque_s((uint32_t)seed), k1 = pt_opaque_s((uint32_t)(seed >> 32));
-#else
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#endif
     c[0] = pixel; c[1] = sample; c[2] = bounce; c[3] = blk;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {

@@ -12,6 +12,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -47,6 +49,7 @@ struct RenderK {
     uint32_t split, split_log2;
     uint32_t npix;
     int32_t out_f64;
+    uint32_t out_stride;   // elements between output rows (pt_render_params.out_row_stride)
     // single kernel, launch drain: the pixels from tail_pix on (the image's
     // top rows, dispatched last) get 2^tail_log2 lanes each, from lane
     // tail_lane (a multiple of 64) on; tail_pix = npix: none
@@ -119,7 +122,7 @@ __device__ __forceinline__ void store_pixel(const RenderK& R, const SlotJob& j, 
     }
     if (j.valid && j.c == 0) {   // pixel_color_list[i] / how_many_rays, main.py:277
         const double inv = (double)R.spp;
-        const size_t e = ((size_t)(R.n_rows - 1 - j.row_local) * (size_t)R.W + (size_t)j.ix) * 3;
+        const size_t e = (size_t)(R.n_rows - 1 - j.row_local) * (size_t)R.out_stride + (size_t)j.ix * 3;
         if (R.out_f64) {
             double* o = (double*)out + e;
             o[0] = acc.x / inv; o[1] = acc.y / inv; o[2] = acc.z / inv;
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(256, PT_RENDER_WAVES) void k_render(SceneK S, Rende
         int tri0 = -1;
         // (a pixel's lanes are all valid or all invalid, and split <= spp
         // gives every lane samples: the whole group takes this branch)
-        if (PT_PRIMARY_SHARED && !FORCE64 && !BVH && split >= PT_PRIMARY_SHARED) {
+        if (PT_PRIMARY_SHARED && !FORCE64 && !COUNT && !BVH && split >= PT_PRIMARY_SHARED) {
             if (R.bounces > 0) tri0 = primary_shared(S, eye, d0, c, split, sp, &P0);
         } else if (ns > 0 && R.bounces > 0) {
             tri0 = closest<FORCE64, false, BVH>(S, eye, d0, -1, sp, &P0, &cnt, true);
@@ -549,164 +552,6 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
     flush_walk_counts<COUNT>(c_q, c_nodes, c_units, wc);
 }
 
-#ifndef PT_GRID_FLAT
-#define PT_GRID_FLAT 1
-#endif
-#ifndef PT_GRID_DUP   // experiment: records duplicated in cell order (gunitc), prefetched
-#define PT_GRID_DUP 0
-#endif
-#ifndef PT_GRID_LA    // experiment (with PT_GRID_DUP): the next cell's range loaded a cell ahead
-#define PT_GRID_LA 0
-#endif
-// The shadow walks through the uniform grid (pt_path.h "grid shadow walks",
-// pt_prepare.h build_grid): one ray per work-item, persistent as k_wf_shadow.
-// A turn tests one unit of the lane's current cell (moving on through
-// emptied cells first), so the lanes of a wave stay busy whatever their
-// cells hold.  COUNT: cells entered as node visits, unit tests as leaf units.
-template <bool UC, bool COUNT>
-__global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow_grid(SceneK S, WfPath* __restrict__ W,
-                                                        WfShadowQ* __restrict__ SQ,
-                                                        const int32_t* __restrict__ list, int32_t* counters,
-                                                        unsigned long long* wc) {
-    uint32_t c_q = 0, c_cells = 0, c_units = 0;
-    const int32_t count = counters[0];
-    int32_t cb = 0, ce = 0;   // this wave's claimed list positions (wf_fetch)
-    int32_t slot = -1;
-    bool exhausted = false;
-    Shadow1 r;
-    F3 o32, inv;
-    int ogrp = -1;
-    GridTrav G;
-    G.live = false;
-#if PT_GRID_DUP
-    UnitC pre{};
-#endif
-#if PT_GRID_DUP && PT_GRID_LA
-    bool nlive = false;
-    int ncur = 0, nend = 0;
-#endif
-    while (true) {
-        const bool need = slot < 0 && !exhausted;
-        if (__any(need)) {
-            const int32_t i = wf_fetch(need, &counters[1], cb, ce);
-            if (need) {
-                if (i < count) {
-                    const int32_t e = list[i];
-                    slot = e >> 2;
-                    if (COUNT) ++c_q;
-                    wf_get_shadow1(SQ[slot], e & 3, &o32, &ogrp, &r);
-                    inv = rcp_dir(r.d32);
-                    g_init(G, S, o32, r.d32, inv, r.hhi, shadow1_open(S, r));
-                    if (COUNT && G.live) ++c_cells;
-#if PT_GRID_DUP
-                    if (G.live && G.cur < G.end) pre = S.gunitc[G.cur];
-#endif
-#if PT_GRID_DUP && PT_GRID_LA
-                    nlive = G.live && g_adv(G, S, o32, inv);
-                    if (nlive) {
-                        const int c = (G.c[2] * S.g_n[1] + G.c[1]) * S.g_n[0] + G.c[0];
-                        ncur = S.gcell[c];
-                        nend = S.gcell[c + 1];
-                    }
-#endif
-                } else {
-                    exhausted = true;
-                }
-            }
-        }
-        if (__all(slot < 0)) break;
-        if (slot >= 0) {
-#if PT_GRID_DUP
-#if PT_GRID_LA
-            // one cell of look-ahead: the DDA cursor G runs a cell ahead and
-            // that cell's range (ncur, nend) is loaded while the current
-            // cell's records are tested
-            if (G.live && G.cur >= G.end) {
-                if (!nlive) {
-                    G.live = false;
-                } else {
-                    G.cur = ncur;
-                    G.end = nend;
-                    if (COUNT) ++c_cells;
-                    if (G.cur < G.end) pre = S.gunitc[G.cur];
-                    nlive = g_adv(G, S, o32, inv);
-                    if (nlive) {
-                        const int c = (G.c[2] * S.g_n[1] + G.c[1]) * S.g_n[0] + G.c[0];
-                        ncur = S.gcell[c];
-                        nend = S.gcell[c + 1];
-                    }
-                }
-            } else if (G.live) {
-                const UnitC rec = pre;
-                ++G.cur;
-                if (G.cur < G.end) pre = S.gunitc[G.cur];
-                if (!g_mailbox(G, rec.t)) {
-                    if (COUNT) ++c_units;
-                    const Spill sp{W[slot].sp, 1};
-                    shadow1_unit(S, unitc_f(S, rec), o32, ogrp, &r, sp);
-                    if (!shadow1_open(S, r)) G.live = false;
-                }
-            }
-#else
-            // the cell's records in cell order, the next one loaded while
-            // this one is tested (UC scenes only: gunitc)
-            if (G.live && G.cur >= G.end) {
-                G.live = g_next(G, S, o32, inv);
-                if (COUNT && G.live) ++c_cells;
-                if (G.live && G.cur < G.end) pre = S.gunitc[G.cur];
-            } else if (G.live) {
-                const UnitC rec = pre;
-                ++G.cur;
-                if (G.cur < G.end) pre = S.gunitc[G.cur];
-                if (!g_mailbox(G, rec.t)) {
-                    if (COUNT) ++c_units;
-                    const Spill sp{W[slot].sp, 1};
-                    shadow1_unit(S, unitc_f(S, rec), o32, ogrp, &r, sp);
-                    if (!shadow1_open(S, r)) G.live = false;
-                }
-            }
-#endif
-            if (!G.live) {
-                wf_put_shadow1(&SQ[slot], r);
-                slot = -1;
-            }
-        }
-    }
-    flush_walk_counts<COUNT>(c_q, c_cells, c_units, wc);
-}
-#else
-#if PT_GRID_FLAT
-            // a turn either moves on one cell or tests one unit (no wave-wide
-            // wait for the lane with the most empty cells in a row)
-            if (G.live && G.cur >= G.end) {
-                G.live = g_next(G, S, o32, inv);
-                if (COUNT && G.live) ++c_cells;
-            } else if (G.live) {
-#else
-            while (G.live && G.cur >= G.end) {   // on to a cell with units left
-                G.live = g_next(G, S, o32, inv);
-                if (COUNT && G.live) ++c_cells;
-            }
-            if (G.live) {
-#endif
-                const int u = S.gref[G.cur++];
-                if (!g_mailbox(G, u)) {
-                    if (COUNT) ++c_units;
-                    const Spill sp{W[slot].sp, 1};
-                    shadow1_unit(S, bvh_unit<UC>(S, u), o32, ogrp, &r, sp);
-                    if (!shadow1_open(S, r)) G.live = false;
-                }
-            }
-            if (!G.live) {
-                wf_put_shadow1(&SQ[slot], r);
-                slot = -1;
-            }
-        }
-    }
-    flush_walk_counts<COUNT>(c_q, c_cells, c_units, wc);
-}
-#endif
-
 template <bool UC, bool COUNT>
 __global__ __launch_bounds__(256, PT_CLOSEST_WAVES) void k_wf_closest(SceneK S, WfPath* __restrict__ W,
                                                     WfClosestQ* __restrict__ CQ,
@@ -801,6 +646,12 @@ __device__ __forceinline__ bool in_box(F3 o, float x) {
     return fabsf(o.x) <= x && fabsf(o.y) <= x && fabsf(o.z) <= x;
 }
 
+// pt_signal: one 64-bit flag store after the stream's earlier work, released
+// at system scope (a vector store; the host or a peer polls the flag)
+__global__ __launch_bounds__(64) void k_signal(uint64_t* flag, uint64_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(256) void k_intersect(SceneK S, const double* __restrict__ rays,
                                                    int64_t n, float xs, float xa,
                                                    int32_t* __restrict__ out_tri,
@@ -848,6 +699,7 @@ __global__ __launch_bounds__(256) void k_color(SceneK S, const int32_t* __restri
 // ---------------------------------------------------------------- API --
 struct pt_scene {
     int device = 0;
+    uint64_t fingerprint = 0;   // of the scene descriptor (pt_render_multi: one scene on every handle)
     int n_cu = 256;   // compute units of the device (MI355X: 256 in 8 XCDs)
     HostScene host;
     SceneK dev{};
@@ -907,19 +759,6 @@ static int dev_alloc_copy(T** d, const T* h, size_t n) {
     if (h) HIPCHK(hipMemcpy(*d, h, n * sizeof(T), hipMemcpyHostToDevice));
     return PT_OK;
 }
-
-#if defined(PT_SKIPSTAT)
-// dev builds only (scripts/skip_stats.py): the unit-pass skip counters of pt_path.h
-extern "C" int pt_debug_skip_stats(unsigned long long* out, int reset) {
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(pt_skip_stat), 16 * sizeof(unsigned long long)));
-    if (reset) {
-        unsigned long long z[16] = {};
-        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(pt_skip_stat), z, sizeof(z)));
-    }
-    return PT_OK;
-}
-#endif
 
 #if defined(PT_PHASE_CLOCKS)
 // dev builds only (scripts/phase_clocks.py): the phase clocks of pt_path.h
@@ -981,6 +820,24 @@ int pt_scene_create_on(const pt_scene_desc* desc, int32_t device, pt_scene** out
     return pt_scene_create(desc, out);
 }
 
+// FNV-1a over the descriptor's arrays and constants
+static void fnv(uint64_t* h, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) *h = (*h ^ b[i]) * 0x100000001b3ull;
+}
+static uint64_t scene_fingerprint(const pt_scene_desc* d) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    const size_t T = (size_t)d->n_tri;
+    fnv(&h, &d->n_tri, 3 * sizeof(int32_t));
+    fnv(&h, d->tri_v, 9 * T * sizeof(double));
+    fnv(&h, d->tri_n, 3 * T * sizeof(double));
+    fnv(&h, d->tri_area, T * sizeof(double));
+    fnv(&h, d->tri_obj, T * sizeof(int32_t));
+    fnv(&h, d->mat, 8 * (size_t)d->n_obj * sizeof(double));
+    fnv(&h, d->eye, sizeof(d->eye) + sizeof(d->ortho) + sizeof(d->ambient) + sizeof(d->light_rgb));
+    return h;
+}
+
 int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     if (!out) return fail(PT_EINVAL, "null output handle");
     *out = nullptr;
@@ -991,6 +848,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     std::string err = prepare_scene(desc, &s->host);
     if (!err.empty()) { delete s; return fail(PT_EINVAL, err); }
     if (hipGetDevice(&s->device) != hipSuccess) { delete s; return fail(PT_EHIP, "hipGetDevice failed"); }
+    s->fingerprint = scene_fingerprint(desc);   // (prepare_scene checked the arrays)
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, s->device) == hipSuccess) {
         if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
@@ -1001,7 +859,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         if (prop.multiProcessorCount > 0) s->n_cu = prop.multiProcessorCount;
     }
     HostScene& H = s->host;
-    constexpr int kArrays = 18;
+    constexpr int kArrays = 14;
     const size_t sz[kArrays] = {H.unit.size() * sizeof(UnitF), H.trid.size() * sizeof(TriD),
                                 H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
                                 H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
@@ -1009,14 +867,11 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
                                 H.tri_grp.size() * sizeof(int32_t),
                                 H.bnode.size() * sizeof(BNode), H.bunit.size() * sizeof(UnitF),
                                 H.cnode.size() * sizeof(CNode), H.qnode.size() * sizeof(QNode),
-                                H.bunitc.size() * sizeof(UnitC), H.unit_eye.size() * sizeof(UnitF),
-                                H.unit_lc.size() * sizeof(float), H.gcell.size() * sizeof(int32_t),
-                                H.gref.size() * sizeof(int32_t), H.gunitc.size() * sizeof(UnitC)};
+                                H.bunitc.size() * sizeof(UnitC), H.unit_eye.size() * sizeof(UnitF)};
     const void* src[kArrays] = {H.unit.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
                                 H.mat.data(), H.light_tri.data(), H.light_cum.data(),
                                 H.tri_grp.data(), H.bnode.data(), H.bunit.data(), H.cnode.data(),
-                                H.qnode.data(), H.bunitc.data(), H.unit_eye.data(), H.unit_lc.data(),
-                                H.gcell.data(), H.gref.data(), H.gunitc.data()};
+                                H.qnode.data(), H.bunitc.data(), H.unit_eye.data()};
     size_t off[kArrays], total = 0;
     for (int i = 0; i < kArrays; ++i) { off[i] = total; total += align_up(sz[i]); }
     int rc = PT_OK;
@@ -1045,10 +900,6 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     s->dev.qnode = (const QNode*)(b + off[11]);
     s->dev.bunitc = H.bunitc.empty() ? nullptr : (const UnitC*)(b + off[12]);
     s->dev.unit_eye = (const UnitF*)(b + off[13]);
-    s->dev.unit_lc = (const float*)(b + off[14]);
-    s->dev.gcell = H.gcell.empty() ? nullptr : (const int32_t*)(b + off[15]);
-    s->dev.gref = H.gref.empty() ? nullptr : (const int32_t*)(b + off[16]);
-    s->dev.gunitc = H.gunitc.empty() ? nullptr : (const UnitC*)(b + off[17]);
     s->xb_surf = box_bound(H, false);
     s->xb_all = box_bound(H, true);
     *out = s;
@@ -1062,6 +913,8 @@ int pt_band_rows(const pt_render_params* p, int32_t* rows) {
     return PT_OK;
 }
 
+constexpr uint32_t kKnownFlags = PT_FLAG_RR | PT_FLAG_FORCE_F64 | PT_FLAG_COUNT | PT_FLAG_OUT_F64 |
+                                 PT_FLAG_MEGAKERNEL | PT_FLAG_WALK_COUNT | PT_FLAG_KERNEL_TIMES;
 static int validate(const pt_render_params* p) {
     if (!p) return fail(PT_EINVAL, "null params");
     if (p->width <= 0 || p->height <= 0) return fail(PT_EINVAL, "width/height must be > 0");
@@ -1072,6 +925,17 @@ static int validate(const pt_render_params* p) {
     if (p->sample_begin < 0) return fail(PT_EINVAL, "sample_begin must be >= 0");
     if (p->row_step <= 0 || p->row_phase < 0 || p->row_phase >= p->row_step)
         return fail(PT_EINVAL, "need row_step > 0 and 0 <= row_phase < row_step");
+    if (p->flags & ~kKnownFlags)
+        return fail(PT_EINVAL, "unknown flag bits (bit 7, v4's PT_FLAG_TREE_WALK, is retired)");
+    if (p->out_row_stride != 0 && (int64_t)p->out_row_stride < (int64_t)p->width * 3)
+        return fail(PT_EINVAL, "out_row_stride must be 0 or >= width*3");
+    if (p->lanes_per_pixel != 0) {
+        uint32_t cap = 64;
+        while (cap > 1 && (int32_t)cap > p->spp) cap >>= 1;
+        const int32_t l = p->lanes_per_pixel;
+        if (l < 0 || (l & (l - 1)) != 0 || l > (int32_t)cap)
+            return fail(PT_EINVAL, "lanes_per_pixel must be 0 or a power of two <= min(64, spp)");
+    }
     return PT_OK;
 }
 
@@ -1233,18 +1097,9 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
             else hipLaunchKernelGGL((k_wf_closest<false, false>), dim3(cl_blocks), dim3(256), 0, on, s->dev, W, q, l, counters + 2, PT_WF_THR_CLOSEST, wc + 3, ovf_cr, ovf_cd, ws);
         }
     };
-    const bool use_grid = s->dev.gcell && (!PT_GRID_DUP || s->dev.gunitc) && !(flags & PT_FLAG_TREE_WALK);
     auto shadow_walk = [&](hipStream_t on) {
         const int32_t* l = lists;
-        if (use_grid) {
-            if (s->dev.bunitc) {
-                if (wcount) hipLaunchKernelGGL((k_wf_shadow_grid<true, true>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, wc);
-                else hipLaunchKernelGGL((k_wf_shadow_grid<true, false>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, wc);
-            } else {
-                if (wcount) hipLaunchKernelGGL((k_wf_shadow_grid<false, true>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, wc);
-                else hipLaunchKernelGGL((k_wf_shadow_grid<false, false>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, wc);
-            }
-        } else if (s->dev.bunitc) {
+        if (s->dev.bunitc) {
             if (wcount) hipLaunchKernelGGL((k_wf_shadow<true, true>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc, ovf_s);
             else hipLaunchKernelGGL((k_wf_shadow<true, false>), dim3(sh_blocks), dim3(256), 0, on, s->dev, W, SQ, l, counters, PT_WF_THR_SHADOW, wc, ovf_s);
         } else {
@@ -1319,9 +1174,9 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
 
 int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void* stream,
                      pt_stats* stats) {
-    if (!s) return fail(PT_EINVAL, "null scene");
     int rc = validate(p);
     if (rc) return rc;
+    if (!s) return fail(PT_EINVAL, "null scene");
     int32_t first = 0, rows = 0;
     band_layout(p, &first, &rows);
     if (rows == 0) return PT_OK;
@@ -1336,8 +1191,11 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     R.sample_begin = p->sample_begin;
     R.out_f64 = (p->flags & PT_FLAG_OUT_F64) ? 1 : 0;
     R.npix = (uint32_t)rows * (uint32_t)p->width;
-    R.split = choose_split((uint64_t)p->width * (uint64_t)p->height, (uint64_t)R.npix, p->spp,
-                           s->dev.n_bnode > 0, min_lanes_of(s->n_cu));
+    R.out_stride = p->out_row_stride ? (uint32_t)p->out_row_stride : (uint32_t)p->width * 3u;
+    R.split = p->lanes_per_pixel > 0
+                  ? (uint32_t)p->lanes_per_pixel
+                  : choose_split((uint64_t)p->width * (uint64_t)p->height, (uint64_t)R.npix, p->spp,
+                                 s->dev.n_bnode > 0, min_lanes_of(s->n_cu));
     R.split_log2 = 0;
     while ((1u << R.split_log2) < R.split) ++R.split_log2;
     R.tail_pix = R.npix;
@@ -1427,16 +1285,17 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
 }
 
 int pt_render(pt_scene* s, const pt_render_params* p, void* out_host, pt_stats* stats) {
-    if (!s) return fail(PT_EINVAL, "null scene");
     int rc = validate(p);
     if (rc) return rc;
+    if (!s) return fail(PT_EINVAL, "null scene");
     int32_t first = 0, rows = 0;
     band_layout(p, &first, &rows);
     if (rows == 0) return PT_OK;
     if (!out_host) return fail(PT_EINVAL, "null output");
     DeviceGuard g(s->device);
     const size_t elem = (p->flags & PT_FLAG_OUT_F64) ? sizeof(double) : sizeof(float);
-    const size_t bytes = (size_t)rows * p->width * 3 * elem;
+    const size_t row_bytes = (size_t)p->width * 3 * elem;
+    const size_t bytes = (size_t)rows * row_bytes;
     if (bytes > s->out_cap) {
         if (s->out_dev) (void)hipFree(s->out_dev);
         s->out_dev = nullptr;
@@ -1444,9 +1303,15 @@ int pt_render(pt_scene* s, const pt_render_params* p, void* out_host, pt_stats* 
         HIPCHK(hipMalloc(&s->out_dev, bytes));
         s->out_cap = bytes;
     }
-    rc = pt_render_device(s, p, s->out_dev, s->stream, stats);
+    pt_render_params q = *p;   // packed in the staging buffer, strided on the host
+    q.out_row_stride = 0;
+    rc = pt_render_device(s, &q, s->out_dev, s->stream, stats);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(out_host, s->out_dev, bytes, hipMemcpyDeviceToHost, s->stream));
+    if (p->out_row_stride == 0 || (size_t)p->out_row_stride * elem == row_bytes)
+        HIPCHK(hipMemcpyAsync(out_host, s->out_dev, bytes, hipMemcpyDeviceToHost, s->stream));
+    else
+        HIPCHK(hipMemcpy2DAsync(out_host, (size_t)p->out_row_stride * elem, s->out_dev, row_bytes,
+                                row_bytes, (size_t)rows, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
     return PT_OK;
 }
@@ -1469,14 +1334,33 @@ static_assert(sizeof(pt_stats) == 17 * 8 + 3 * 8, "add_stats covers every pt_sta
 
 extern "C" {
 
+// Waits for the work already queued on the first n handles' streams (the
+// error path of pt_render_multi: asynchronous band renders and copies of
+// devices launched before the failing one must not outlive the call).
+static void drain(pt_scene* const* scenes, int32_t n) {
+    for (int32_t i = 0; i < n; ++i) {
+        DeviceGuard g(scenes[i]->device);
+        (void)hipStreamSynchronize(scenes[i]->stream);
+    }
+}
+
 int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* p, void* out_host,
                     pt_stats* stats) {
     if (!scenes || n <= 0) return fail(PT_EINVAL, "need n >= 1 scene handles");
-    for (int32_t i = 0; i < n; ++i)
+    for (int32_t i = 0; i < n; ++i) {
         if (!scenes[i]) return fail(PT_EINVAL, "null scene handle");
+        if (scenes[i]->fingerprint != scenes[0]->fingerprint)
+            return fail(PT_EINVAL, "handle " + std::to_string(i) + " holds another scene than handle 0");
+    }
     int rc = validate(p);
     if (rc) return rc;
+    // fault injection for the tests of the error path (tests/test_gpu.py):
+    // PT_FAULT_INJECT_MULTI=i makes dealing band i fail after bands 0..i-1
+    // were launched
+    const char* fi = getenv("PT_FAULT_INJECT_MULTI");
+    const int32_t fail_at = fi ? (int32_t)atoi(fi) : -1;
     if (p->row_step != 1) return fail(PT_EINVAL, "pt_render_multi deals out the rows itself: row_step must be 1");
+    if (p->out_row_stride != 0) return fail(PT_EINVAL, "pt_render_multi writes the packed layout: out_row_stride must be 0");
     int32_t first = 0, total = 0;
     band_layout(p, &first, &total);
     if (total == 0) return PT_OK;
@@ -1490,7 +1374,8 @@ int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* 
     if (stats) memset(stats, 0, sizeof(*stats));
     std::vector<pt_render_params> bp(n);
     std::vector<int32_t> rows(n, 0);
-    // 1. every device renders its band into its staging buffer (asynchronous)
+    // 1. every device renders its band into its staging buffer (asynchronous);
+    // a failure drains the devices launched so far (and this one) first
     for (int32_t i = 0; i < n; ++i) {
         pt_scene* s = scenes[i];
         bp[i] = *p;
@@ -1501,19 +1386,37 @@ int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* 
         int32_t f = 0;
         band_layout(&bp[i], &f, &rows[i]);
         if (rows[i] == 0) continue;
-        DeviceGuard g(s->device);
-        const size_t bytes = (size_t)rows[i] * row_bytes;
-        if (bytes > s->out_cap) {
-            if (s->out_dev) (void)hipFree(s->out_dev);
-            s->out_dev = nullptr;
-            s->out_cap = 0;
-            HIPCHK(hipMalloc(&s->out_dev, bytes));
-            s->out_cap = bytes;
+        int rci = PT_OK;
+        {
+            DeviceGuard g(s->device);
+            const size_t bytes = (size_t)rows[i] * row_bytes;
+            if (bytes > s->out_cap) {
+                // (the handle's previous work may still read or write it)
+                if (hipStreamSynchronize(s->stream) != hipSuccess) {
+                    rci = fail(PT_EHIP, "hipStreamSynchronize before growing a staging buffer failed");
+                } else {
+                    if (s->out_dev) (void)hipFree(s->out_dev);
+                    s->out_dev = nullptr;
+                    s->out_cap = 0;
+                    if (hipMalloc(&s->out_dev, bytes) != hipSuccess)
+                        rci = fail(PT_ENOMEM, "hipMalloc band staging buffer");
+                    else
+                        s->out_cap = bytes;
+                }
+            }
+            if (rci == PT_OK && i == fail_at) rci = fail(PT_EHIP, "fault injected (PT_FAULT_INJECT_MULTI)");
+            if (rci == PT_OK) {
+                pt_stats st;
+                rci = pt_render_device(s, &bp[i], s->out_dev, s->stream, (count && stats) ? &st : nullptr);
+                if (rci == PT_OK && count && stats) add_stats(stats, st);
+            }
         }
-        pt_stats st;
-        rc = pt_render_device(s, &bp[i], s->out_dev, s->stream, (count && stats) ? &st : nullptr);
-        if (rc) return rc;
-        if (count && stats) add_stats(stats, st);
+        if (rci != PT_OK) {
+            const std::string msg = g_err;
+            drain(scenes, i + 1);
+            g_err = "device " + std::to_string(i) + ": " + msg;
+            return rci;
+        }
     }
     // 2. each band lands in its rows of the host frame: band row j (launch
     // order, highest iy first) is frame row (re-1-iy) = (re-1-iy_top) + j*n
@@ -1525,13 +1428,65 @@ int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* 
         int32_t iy_top = re - 1;
         while (((iy_top % n) + n) % n != phase) --iy_top;
         char* dst = (char*)out_host + (size_t)(re - 1 - iy_top) * row_bytes;
-        HIPCHK(hipMemcpy2DAsync(dst, (size_t)n * row_bytes, s->out_dev, row_bytes, row_bytes,
-                                (size_t)rows[i], hipMemcpyDeviceToHost, s->stream));
+        if (hipMemcpy2DAsync(dst, (size_t)n * row_bytes, s->out_dev, row_bytes, row_bytes, (size_t)rows[i],
+                             hipMemcpyDeviceToHost, s->stream) != hipSuccess) {
+            drain(scenes, n);
+            return fail(PT_EHIP, "hipMemcpy2DAsync of device " + std::to_string(i) + "'s band failed");
+        }
     }
+    int rc_sync = PT_OK;
     for (int32_t i = 0; i < n; ++i) {
         DeviceGuard g(scenes[i]->device);
-        HIPCHK(hipStreamSynchronize(scenes[i]->stream));
+        if (hipStreamSynchronize(scenes[i]->stream) != hipSuccess && rc_sync == PT_OK)
+            rc_sync = fail(PT_EHIP, "hipStreamSynchronize of device " + std::to_string(i) + " failed");
     }
+    return rc_sync;
+}
+
+int pt_host_map(void* host, uint64_t bytes, void** dev_ptr) {
+    if (!host || !dev_ptr || bytes == 0) return fail(PT_EINVAL, "need host, bytes > 0 and dev_ptr");
+    *dev_ptr = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(PT_ENODEV, "no HIP device visible (the MI355X path needs a gfx950 GPU)");
+    HIPCHK(hipHostRegister(host, (size_t)bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    void* d = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&d, host, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(host);
+        return fail(PT_EHIP, std::string("hipHostGetDevicePointer failed: ") + hipGetErrorString(e));
+    }
+    *dev_ptr = d;
+    return PT_OK;
+}
+
+int pt_host_unmap(void* host) {
+    if (!host) return fail(PT_EINVAL, "null host pointer");
+    HIPCHK(hipHostUnregister(host));
+    return PT_OK;
+}
+
+int pt_signal(uint64_t* flag_dev, uint64_t value, void* stream) {
+    if (!flag_dev || ((uintptr_t)flag_dev & 7u)) return fail(PT_EINVAL, "need an 8-byte aligned flag");
+    hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, (hipStream_t)stream, flag_dev, value);
+    HIPCHK(hipGetLastError());
+    return PT_OK;
+}
+
+int pt_wait_flags(const uint64_t* flags, int32_t n, int32_t stride, uint64_t value, double timeout_s) {
+    if (!flags || n < 0 || stride <= 0) return fail(PT_EINVAL, "need flags, n >= 0, stride > 0");
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        int32_t i = 0;
+        while (i < n && __atomic_load_n(&flags[(size_t)i * stride], __ATOMIC_RELAXED) >= value) ++i;
+        if (i == n) break;
+        if ((spin & 1023u) == 1023u &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+            return fail(PT_ETIMEOUT, "pt_wait_flags: flag " + std::to_string(i) + " below " +
+                                         std::to_string(value) + " after " + std::to_string(timeout_s) + " s");
+        __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
     return PT_OK;
 }
 

@@ -290,43 +290,9 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double u[12], ShadowS
 #ifndef PT_QUAD
 #define PT_QUAD 1
 #endif
-// Experiment switches (both exact, both measured
-// slower — 5.68 / 5.70 vs 5.62 ms — so both are off): the light-side cull of
-// the uniform units' shadow tests, and the closest ray's skip of a unit
-// certainly beyond the current winner.  Wave-level counts from a
-// -DPT_SKIPSTAT build (scripts/skip_stats.py): the cull removes 19% of the
-// shadow parts (lane level: 62% of (lane, unit) pairs), the closest skip 2.4%.
-#ifndef PT_LCULL
-#define PT_LCULL 0
-#endif
-#ifndef PT_CSKIP
-#define PT_CSKIP 0
-#endif
-// a lower bound any test of a unit could add (f32: at - dt; f64 fallback:
-// sqrtf(sqd)(1 - 1e-6) >= (at - dt)(1 - 1.2e-6)) is above (at - dt) kCSkip
-constexpr float kCSkip = 1.0f - 4e-6f;
-#if defined(PT_SKIPSTAT) && defined(__HIP__)
-__device__ unsigned long long pt_skip_stat[16];   // (dev builds: the host reads it)
-#endif
-#if defined(PT_SKIPSTAT) && defined(__HIP_DEVICE_COMPILE__)
-// one count per wave (its first active lane) when the wave-uniform c holds
-#define PT_SKIP_EV(i, c)                                                          \
-    do {                                                                          \
-        const bool c_ = (c);                                                      \
-        if (c_ && __lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1)    \
-            atomicAdd(&pt_skip_stat[(i)], 1ull);                                  \
-    } while (0)
-// the number of the wave's active lanes where c holds
-#define PT_SKIP_LANES(i, c)                                                       \
-    do {                                                                          \
-        const unsigned long long b_ = __ballot((c));                              \
-        if (__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1)          \
-            atomicAdd(&pt_skip_stat[(i)], (unsigned long long)__popcll(b_));      \
-    } while (0)
-#else
-#define PT_SKIP_EV(i, c)
-#define PT_SKIP_LANES(i, c)
-#endif
+// (Round 3's light-side cull and closest-skip experiments, both exact and
+// both slower, and their skip counters are no longer in the product; the
+// code is at commit 38ea783, DESIGN.md §11 has the measurements.)
 #ifndef PT_RNG_PERBLOCK
 #define PT_RNG_PERBLOCK 1
 #endif
@@ -411,11 +377,6 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
         const RayPlane p = ray_plane(U, O.h, d, sh->hlo[k], sh->hhi[k]);
         float cm, nm;
         margin_plane(U, p, sh->hlo[k], sh->hhi[k], cop, &cm, &nm);
-#if defined(PT_SKIPSTAT)
-        PT_SKIP_EV(3 + k, true);
-        PT_SKIP_EV(6 + k, !PT_WAVE_ANY(!(nm < 0.0f)));
-        PT_SKIP_LANES(13 + k, nm < 0.0f || (k < 2 && oc[k] > 0.0f));
-#endif
         // nm < 0 (the plane part is a certain miss; nm is never NaN, cop is
         // not) implies cm < 0, so every margin of the ray's triangles is
         // negative or a dropped NaN: no occlusion, no ambiguous test.  The
@@ -450,84 +411,12 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
 }
 
 // The f64 decisions of a unit's ambiguous tests (bits of amb, see
-// fused_unit).  Out of line in the render kernels: the block is large (an
-// eval64 per bit) and runs for few waves, so the unit loop does not carry its
-// registers and code.
-#ifndef PT_FALLBACK_NOINLINE
-#define PT_FALLBACK_NOINLINE 0
-#endif
-#if PT_FALLBACK_NOINLINE && defined(__HIP_DEVICE_COMPILE__)
-#define PT_FALLBACK_ATTR __device__ __attribute__((noinline))
-#else
-#define PT_FALLBACK_ATTR PT_HD
-#endif
-#ifndef PT_FALLBACK_LOOP
-#define PT_FALLBACK_LOOP 0
-#endif
+// fused_unit): one rare block per unit (an eval64 per bit), entered by few
+// waves.
 template <bool FORCE64, bool COUNT, bool MARGIN, int PARTS = 3>
-PT_FALLBACK_ATTR void fused_fallback(const SceneK& S, const UnitF& U, uint32_t amb, ShadowSet* sh,
-                                     ClosestAcc* ca, const Spill& sp, Counters* cnt, float* oc) {
+PT_HD void fused_fallback(const SceneK& S, const UnitF& U, uint32_t amb, ShadowSet* sh,
+                          ClosestAcc* ca, const Spill& sp, Counters* cnt, float* oc) {
     const D3 P = sp.get3(kSpP);
-#if PT_FALLBACK_LOOP
-    if (!FORCE64) {
-        // one eval64 site: each lane walks its own ambiguous tests in bit
-        // order (shadow ray k, triangle i at bit 2k+i; the closest ray's at
-        // 6+i), the order of the nested loops below
-        uint32_t bits = amb;
-        while (bits) {
-            const int bi = __builtin_ctz(bits);
-            bits &= bits - 1u;
-            const int i = bi & 1, k = bi >> 1;
-            const int t = U.t[i];
-            if (bi < 6) {   // shadow ray k
-                const bool occk = MARGIN ? ((k == 0 ? oc[0] : (k == 1 ? oc[1] : oc[2])) > 0.0f)
-                                         : (k == 0 ? sh->occ[0] : (k == 1 ? sh->occ[1] : sh->occ[2]));
-                const int firstk = k == 0 ? sh->first[0] : (k == 1 ? sh->first[1] : sh->first[2]);
-                // decided meanwhile (a lower occluder of this unit, or occlusion)?
-                if (k == kLightSamples - 1 ? ((COUNT ? t : U.obj) >= sh->key2)
-                                           : (COUNT ? (t >= firstk) : occk))
-                    continue;
-                bump<COUNT>(cnt, &Counters::fallbacks, 1);
-                const D3 L = sp.get3(kSpL + 3 * k);
-                D3 Q;
-                double sqd;
-                if (eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
-                    sqd < squared_dist(P, L)) {
-                    if (COUNT && t < firstk) {
-                        if (k == 0) sh->first[0] = t;
-                        else if (k == 1) sh->first[1] = t;
-                        else sh->first[2] = t;
-                    }
-                    if (k == kLightSamples - 1) {
-                        sh->key2 = COUNT ? t : U.obj;
-                        sh->leak = U.obj;
-                    }
-                    if (MARGIN) {
-                        if (k == 0) oc[0] = 1.0f;
-                        else if (k == 1) oc[1] = 1.0f;
-                        else oc[2] = 1.0f;
-                    } else {
-                        if (k == 0) sh->occ[0] = true;
-                        else if (k == 1) sh->occ[1] = true;
-                        else sh->occ[2] = true;
-                    }
-                }
-            } else {   // the closest ray
-                bump<COUNT>(cnt, &Counters::fallbacks, 1);
-                D3 Q;
-                double sqd;
-                float a = INFINITY, b = INFINITY;
-                if (eval64(S.trid[t], P, unit(sp.get3(kSpNd)), &Q, &sqd) && sqd > kZero) {
-                    const float sq = sqrtf((float)sqd);   // |t| to ~1e-7; brackets are 1e-6
-                    a = sq * (1.0f - 1e-6f);
-                    b = sq * (1.0f + 1e-6f);
-                }
-                closest_add(ca, t, a, b);
-            }
-        }
-        return;
-    }
-#endif
     for (int k = 0; k < ((PARTS & 1) ? kLightSamples : 0); ++k) {
         for (int i = 0; i < 2; ++i) {
             if (!((amb >> (2 * k + i)) & 1u)) continue;
@@ -585,7 +474,7 @@ template <bool FORCE64, bool COUNT, bool MARGIN = false, int PARTS = 3>
 PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
                       bool do_shadow, bool do_closest, ShadowSet* sh, F3 n32, ClosestAcc* ca,
                       const Spill& sp, Counters* cnt, uint32_t rays = 15u,
-                      float* oc = nullptr, bool ctrace = true) {
+                      float* oc = nullptr) {
     if (!(PARTS & 1)) do_shadow = false;
     if (!(PARTS & 2)) do_closest = false;
     // rays: bit k = shadow ray k, bit 3 = the closest ray (the BVH passes the
@@ -634,22 +523,6 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
     }
     if (!FORCE64 && do_closest && (rays & 8u)) {
         const RayPlane p = ray_plane(U, O.h, n32, INFINITY, INFINITY);
-#if defined(PT_SKIPSTAT)
-        if (MARGIN) {
-            PT_SKIP_EV(9, true);
-            PT_SKIP_EV(10, !PT_WAVE_ANY(ctrace && !((p.at - p.dt) * kCSkip > ca->b1)));
-        }
-#endif
-#if PT_CSKIP
-        // the unit cannot change the closest-hit decision when its |t| is
-        // certainly beyond the current winner's upper bound b1 (every lower
-        // bound a test of it could add, an f64 fallback's included, exceeds
-        // b1: neither the winner nor the certainty test b1 < a2 changes,
-        // closest_add / closest_finish); skipped when that holds on every
-        // lane that traces
-        if (MARGIN && !PT_WAVE_ANY(ctrace && !((p.at - p.dt) * kCSkip > ca->b1))) goto closest_done;
-#endif
-        {
         bool c0, a0, c1 = false, a1 = false;
         if (MARGIN && PT_QUAD) {   // the render loop's unit form (quad_m)
             const QuadM m = quad_m(U, p, O, n32);
@@ -674,14 +547,7 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
         closest_add(ca, c0 ? U.t[0] : U.t[1], c ? p.at - p.dt : INFINITY,
                     c ? p.at + p.dt : INFINITY);
         amb |= (a0 ? 64u : 0u) | (a1 ? 128u : 0u);
-        }
     }
-#if PT_CSKIP
-closest_done:
-#endif
-#ifdef PT_ABL_NOAMB   // timing ablation only (wrong results)
-    if (!FORCE64) amb = 0;
-#endif
     amb &= ((PARTS & 1) ? 0x3fu : 0u) | ((PARTS & 2) ? 0xc0u : 0u);
     if (amb) fused_fallback<FORCE64, COUNT, MARGIN, PARTS>(S, U, amb, sh, ca, sp, cnt, oc);   // rare (FORCE64: every shadow test) — decide in f64
 }
@@ -1550,88 +1416,6 @@ PT_HD void s1_units(const ShadowTrav1& T, const SceneK& S, Shadow1* r, const Spi
         shadow1_unit(S, bvh_unit<UC>(S, u0 + i), T.o32, T.ogrp, r, sp);
 }
 
-// ------------------------------------------------- grid shadow walks --
-// One shadow ray marched through the uniform grid over the BVH units
-// (pt_prepare.h build_grid: exactness argument there), cell by cell along
-// t in [-R, R] (two-sided, main.py:42-47), testing each cell's units with the
-// tree walk's leaf test (shadow1_unit).  A unit listed in several cells is
-// tested once per cell: any-hit results do not change (ray 2 keeps its lowest
-// occluding object).
-struct GridTrav {
-    int c[3];      // current cell
-    float tn[3];   // line parameter where the line leaves the cell, per axis
-    float tend;    // end of the clipped segment
-    int cur, end;  // the current cell's units: gref[cur .. end)
-    int last0, last1;   // the last two units tested (a unit spans a few cells)
-    bool live;
-};
-// true when unit u was one of the last two tested (its test would repeat);
-// else records it
-PT_HD bool g_mailbox(GridTrav& G, int u) {
-    if (u == G.last0 || u == G.last1) return true;
-    G.last1 = G.last0;
-    G.last0 = u;
-    return false;
-}
-PT_HD float g_cross(const SceneK& S, int a, int ci, float o, float inv) {
-    // the cell boundary the line crosses next on axis a (upper when inv > 0)
-    const float b = fmaf((float)(inv > 0.0f ? ci + 1 : ci), S.g_h, S.g_org[a]);
-    return (b - o) * inv;
-}
-PT_HD void g_load(GridTrav& G, const SceneK& S) {
-    const int c = (G.c[2] * S.g_n[1] + G.c[1]) * S.g_n[0] + G.c[0];
-    G.cur = S.gcell[c];
-    G.end = S.gcell[c + 1];
-}
-PT_HD void g_init(GridTrav& G, const SceneK& S, F3 o, F3 d, F3 inv, float R, bool open) {
-    const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, ii[3] = {inv.x, inv.y, inv.z};
-    float ta = -R, tb = R;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {   // clip the segment to the grid box
-        const float g1 = fmaf((float)S.g_n[a], S.g_h, S.g_org[a]);
-        const float t0 = (S.g_org[a] - oo[a]) * ii[a], t1 = (g1 - oo[a]) * ii[a];
-        ta = fmaxf(ta, fminf(t0, t1));
-        tb = fminf(tb, fmaxf(t0, t1));
-    }
-    G.live = open && ta <= tb;
-    G.tend = tb;
-    G.cur = G.end = 0;
-    G.last0 = G.last1 = -1;
-    const float ih = 1.0f / S.g_h;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float p = fmaf(ta, dd[a], oo[a]);
-        int ci = (int)floorf((p - S.g_org[a]) * ih);
-        ci = ci < 0 ? 0 : (ci >= S.g_n[a] ? S.g_n[a] - 1 : ci);
-        G.c[a] = ci;
-        G.tn[a] = g_cross(S, a, ci, oo[a], ii[a]);
-    }
-    if (G.live) g_load(G, S);
-}
-// to the next cell along the line; false past the segment's end or the grid
-PT_HD bool g_adv(GridTrav& G, const SceneK& S, F3 o, F3 inv);
-PT_HD bool g_next(GridTrav& G, const SceneK& S, F3 o, F3 inv) {
-    if (!g_adv(G, S, o, inv)) return false;
-    g_load(G, S);
-    return true;
-}
-// the DDA step alone (no load of the new cell's range)
-PT_HD bool g_adv(GridTrav& G, const SceneK& S, F3 o, F3 inv) {
-    const int a = (G.tn[0] <= G.tn[1]) ? (G.tn[0] <= G.tn[2] ? 0 : 2) : (G.tn[1] <= G.tn[2] ? 1 : 2);
-    const float ia = a == 0 ? inv.x : (a == 1 ? inv.y : inv.z);
-    const float oa = a == 0 ? o.x : (a == 1 ? o.y : o.z);
-    const float t = a == 0 ? G.tn[0] : (a == 1 ? G.tn[1] : G.tn[2]);
-    if (!(t <= G.tend)) return false;
-    int ci = (a == 0 ? G.c[0] : (a == 1 ? G.c[1] : G.c[2])) + (ia > 0.0f ? 1 : -1);
-    const int na = a == 0 ? S.g_n[0] : (a == 1 ? S.g_n[1] : S.g_n[2]);
-    if (ci < 0 || ci >= na) return false;
-    const float tn = g_cross(S, a, ci, oa, ia);
-    if (a == 0) { G.c[0] = ci; G.tn[0] = tn; }
-    else if (a == 1) { G.c[1] = ci; G.tn[1] = tn; }
-    else { G.c[2] = ci; G.tn[2] = tn; }
-    return true;
-}
-
 // Standalone query (primary rays, the batched intersect_objects API).  d need
 // not be normalised (utils.py:110).  ogrp: coplanar group of the triangle the
 // origin lies on (-1: none).
@@ -1889,39 +1673,10 @@ PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& 
             for (int u = 0; u < S.n_obj_unit; ++u) {
                 const UnitF U = S.unit[u];
                 const OriginU O = PT_QUAD ? origin_q(U, o32u) : origin_u(U, o32u);
-#ifdef PT_ABL_NOSHADOW   // timing ablation only (wrong results)
-                const bool do_shadow = false;
-#else
-#if PT_LCULL
-                // a lane needs no shadow test of this unit when its three rays
-                // are occluded (ray 2: by an object <= this one, scene order),
-                // its origin is on the unit's plane (certain misses) or the
-                // light-side cull holds for every light point (pt_prepare.h
-                // light_cull): the wave skips the unit's shadow part,
-                // plane parts included, when no lane needs it
-                const float lc0 = S.unit_lc[2 * u], lc1 = S.unit_lc[2 * u + 1];
-                const bool lane_off = (oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f) |
-                                      (U.grp == ogrp) | (O.h > lc0) | (O.h < lc1);
-                const bool do_shadow = PT_WAVE_ANY(!lane_off);
-#else
                 const bool do_shadow =
                     PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));
-#endif
-#if defined(PT_SKIPSTAT)
-                {
-                    const float lc0s = S.unit_lc[2 * u], lc1s = S.unit_lc[2 * u + 1];
-                    PT_SKIP_EV(0, true);
-                    PT_SKIP_EV(1, PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f)));
-                    PT_SKIP_EV(2, PT_WAVE_ANY(!((oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f) |
-                                                (U.grp == ogrp) | (O.h > lc0s) | (O.h < lc1s))));
-                    PT_SKIP_LANES(11, true);
-                    PT_SKIP_LANES(12, (oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f) |
-                                          (U.grp == ogrp) | (O.h > lc0s) | (O.h < lc1s));
-                }
-#endif
-#endif
                 fused_unit<FORCE64, COUNT, true>(S, U, O, U.grp == ogrp, do_shadow, any_trace,
-                                                 &sh, n32, &ca, sp, cnt, 15u, oc, trace);
+                                                 &sh, n32, &ca, sp, cnt, 15u, oc);
             }
 #pragma unroll
             for (int k = 0; k < kLightSamples; ++k) sh.occ[k] = oc[k] > 0.0f;
@@ -1940,9 +1695,7 @@ PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& 
             const F3 o32 = to_f3(P - ld3(S.center));   // the BVH's frame
             const bool ordered = !FORCE64 && S.bvh_depth < kBvhStack;
             if (ordered) {
-#ifndef PT_ABL_NOBVHSHADOW
                 bvh_shadow<COUNT>(S, o32, ogrp, &sh, sp, cnt);
-#endif
                 if (trace) bvh_closest<COUNT>(S, o32, ogrp, n32, &ca, sp, cnt);
             } else {
                 bvh_pass<FORCE64, COUNT>(S, o32, ogrp, true, !FORCE64 && trace, &sh, n32, &ca, sp,

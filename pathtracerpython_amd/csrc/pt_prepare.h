@@ -32,10 +32,6 @@ struct HostScene {
     std::vector<Mat> mat;
     std::vector<int32_t> light_tri;
     std::vector<double> light_cum;
-    std::vector<float> unit_lc;   // [2 n_obj_unit] light_cull thresholds
-    std::vector<int32_t> gcell;   // grid CSR starts (build_grid), empty: no grid
-    std::vector<int32_t> gref;
-    std::vector<UnitC> gunitc;    // bunitc[gref[i]] (PT_GRID_DUP)
     SceneK k{};   // pointers unset; constants filled
 };
 
@@ -180,14 +176,22 @@ struct BvhBuilder {
 // walk of the subtree can hold (3 per level at most).
 struct QBuilder {
     HostScene* H;
+    double X;   // the BVH frame's half extent (the boxes' inflation is 64 u X)
     struct Child { int32_t ref; float lo[3], hi[3]; };
     static double area(const Child& c) {
         const double e0 = (double)c.hi[0] - c.lo[0], e1 = (double)c.hi[1] - c.lo[1],
                      e2 = (double)c.hi[2] - c.lo[2];
         return e0 * e1 + e1 * e2 + e2 * e0;
     }
-    // one axis: grid origin / step / codes with exact f32 decode
-    static bool quantise(const Child* ch, int n, int a, QNode* Q) {
+    // one axis: grid origin / step / codes with exact f32 decode.  An absent
+    // child is the empty box lo 255, hi 0: a line's slab parameters on the
+    // axis are fma(255, A, B) and B (A = step inv, B = (org - o) inv), and the
+    // walks test no child reference, so the box must stay empty after
+    // rounding: 255 step has to exceed half an ulp of |org - o| <= 4 X, i.e.
+    // 255 step >= 2^-20 X (4x margin).  The 64 u X inflation of every box
+    // already gives 255 step >= 2^-19 X; the check keeps it a checked fact
+    // (a node that failed it would send the scene to the single kernel).
+    static bool quantise(const Child* ch, int n, int a, QNode* Q, double X) {
         double plo = INFINITY, phi = -INFINITY;
         for (int c = 0; c < n; ++c) { plo = std::min(plo, (double)ch[c].lo[a]); phi = std::max(phi, (double)ch[c].hi[a]); }
         int e = (int)floor(log2(std::max(phi - plo, 1e-30) / 255.0)) - 1;
@@ -209,6 +213,7 @@ struct QBuilder {
                 hi |= (uint32_t)qh << (8 * c);
             }
             if (!ok) continue;
+            if (n < 4 && !(255.0 * step >= ldexp(X, -20))) return false;
             for (int c = n; c < 4; ++c) lo |= 255u << (8 * c);   // no child: an empty box
             Q->org[a] = (float)org;
             Q->ex |= (uint32_t)(e + 127) << (8 * a);
@@ -245,7 +250,7 @@ struct QBuilder {
         QNode Q{};
         for (int c = 0; c < 4; ++c) Q.ref[c] = kNoRef;
         for (int a = 0; a < 3; ++a)
-            if (!quantise(ch.data(), (int)ch.size(), a, &Q)) failed = true;
+            if (!quantise(ch.data(), (int)ch.size(), a, &Q, X)) failed = true;
         int deepest = 0;
         for (int c = 0; c < (int)ch.size() && !failed; ++c) {
             int sub = 0;
@@ -324,7 +329,7 @@ inline void build_bvh(HostScene* H, double X) {
         C.c1 = ref(b);
     }
     K.bvh_root = ref(0);
-    QBuilder QB{H};
+    QBuilder QB{H, X};
     int qs = 0;
     const int32_t qr = QB.build(K.bvh_root, &qs);
     if (!QB.failed) {
@@ -358,195 +363,6 @@ inline float f32_up(double x) {   // round to f32, never below x (x >= 0)
     float f = (float)x;
     if ((double)f < x) f = nextafterf(f, INFINITY);
     return f;
-}
-
-// Uniform grid over the BVH units for the one-ray shadow walks
-// (k_wf_shadow_grid, pt_path.h "grid walks").  A shadow ray is a line segment
-// |t| <= R (main.py:42-47, two-sided); a grid marches it cell by cell and tests
-// each cell's units, which for a mesh of many small triangles spread through a
-// volume (K5) costs far fewer instructions than a tree walk.  Exactness: a unit
-// is listed in every cell its box, inflated by delta = 128 u X, overlaps.  The
-// march follows the f32 line (centred origin, f32 direction: within ~20 u X of
-// the exact line for |t| <= 2 sqrt(3) X, as for the BVH's slab tests) and at
-// parameter t sits in a cell that the f32 line occupies up to the rounding of
-// the boundary crossings (a few u X), so every point where the reference's
-// line meets a unit is within delta of a visited cell's part of the line: the
-// unit is listed there.  Units are tested with the same verdicts as the tree
-// walk's leaves, each result decided the same way whatever the order (any
-// occluder closes rays 0 and 1; ray 2 keeps its lowest occluding object), so the
-// framebuffer is bit for bit the tree walk's.  Cell size: about
-// PT_GRID_DENSITY units per cell; no grid when the mesh packs too many units
-// into one cell (a grid pays for itself on volumes of small triangles).
-//
-// Measured (round 3, K5 at 1024^2 x 256 spp): bit for bit the
-// tree walk's frame, but the shadow walks take 2029-2947 ms per render
-// against the tree's 603 (densities 0.125-2 units per cell: 23-58 cells and
-// 23-91 unit tests per ray, each cell and each unit one dependent load, vs
-// ~55 dependent node / leaf loads per ray in the tree).  So the library does
-// not build it (PT_GRID 0); the host check build (tests/hostcheck) does and
-// checks the grid walk against the tree walk bit for bit.
-#ifndef PT_GRID
-#define PT_GRID 0
-#endif
-#ifndef PT_GRID_DENSITY
-#define PT_GRID_DENSITY 0.5
-#endif
-#ifndef PT_GRID_MAX_CELL
-#define PT_GRID_MAX_CELL 64
-#endif
-inline void build_grid(HostScene* H, const pt_scene_desc* d, double X) {
-    SceneK& K = H->k;
-    H->gcell.clear();
-    H->gref.clear();
-    H->gunitc.clear();
-    K.g_org[0] = K.g_org[1] = K.g_org[2] = 0.f;
-    K.g_h = 0.f;
-    K.g_n[0] = K.g_n[1] = K.g_n[2] = 0;
-    K.n_gref = 0;
-    const int N = (int)H->bunit.size();
-    if (!PT_GRID || N == 0) return;
-    const double u = 1.0 / 16777216.0, delta = 128.0 * u * X;
-    const D3 C = d3(K.center[0], K.center[1], K.center[2]);
-    std::vector<double> box(6 * (size_t)N);
-    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = 0; i < N; ++i) {
-        const UnitF& U = H->bunit[i];
-        double* b = &box[6 * (size_t)i];
-        for (int a = 0; a < 3; ++a) { b[a] = INFINITY; b[3 + a] = -INFINITY; }
-        for (int m = 0; m < U.count; ++m)
-            for (int v = 0; v < 3; ++v) {
-                const D3 x = tri_vertex(d, U.t[m], v) - C;
-                const double xa[3] = {x.x, x.y, x.z};
-                for (int a = 0; a < 3; ++a) {
-                    b[a] = std::min(b[a], xa[a] - delta);
-                    b[3 + a] = std::max(b[3 + a], xa[a] + delta);
-                }
-            }
-        for (int a = 0; a < 3; ++a) {
-            if (!(b[a] <= b[3 + a]) || !std::isfinite(b[a]) || !std::isfinite(b[3 + a])) return;
-            lo[a] = std::min(lo[a], b[a]);
-            hi[a] = std::max(hi[a], b[3 + a]);
-        }
-    }
-    double vol = 1.0;
-    for (int a = 0; a < 3; ++a) vol *= std::max(hi[a] - lo[a], 1e-6 * X + 1e-30);
-    double h = std::cbrt(vol * PT_GRID_DENSITY / N);
-    int n[3];
-    float G0[3], hf = 0.f;
-    for (int tries = 0;; ++tries) {
-        if (tries > 64) return;
-        hf = f32_upb(h);
-        double cells = 1.0;
-        for (int a = 0; a < 3; ++a) {
-            G0[a] = f32_down(lo[a]);
-            n[a] = std::max(1, (int)std::ceil((hi[a] - (double)G0[a]) / (double)hf));
-            while ((double)G0[a] + (double)n[a] * (double)hf < hi[a]) ++n[a];
-            cells *= n[a];
-        }
-        if (n[0] <= 1024 && n[1] <= 1024 && n[2] <= 1024 && cells <= (double)(1 << 24)) break;
-        h *= 1.25;
-    }
-    const int64_t nc = (int64_t)n[0] * n[1] * n[2];
-    std::vector<int32_t> cnt(nc + 1, 0);
-    auto range = [&](const double* b, int a, int* i0, int* i1) {
-        *i0 = std::min(std::max((int)std::floor((b[a] - (double)G0[a]) / (double)hf), 0), n[a] - 1);
-        *i1 = std::min(std::max((int)std::floor((b[3 + a] - (double)G0[a]) / (double)hf), 0), n[a] - 1);
-    };
-    int64_t total = 0;
-    for (int pass = 0; pass < 2; ++pass) {
-        for (int i = 0; i < N; ++i) {
-            const double* b = &box[6 * (size_t)i];
-            int x0, x1, y0, y1, z0, z1;
-            range(b, 0, &x0, &x1);
-            range(b, 1, &y0, &y1);
-            range(b, 2, &z0, &z1);
-            for (int z = z0; z <= z1; ++z)
-                for (int y = y0; y <= y1; ++y)
-                    for (int x = x0; x <= x1; ++x) {
-                        const int64_t c = ((int64_t)z * n[1] + y) * n[0] + x;
-                        if (pass == 0) ++cnt[c + 1];
-                        else H->gref[cnt[c]++] = i;
-                    }
-        }
-        if (pass == 0) {
-            int maxc = 0;
-            for (int64_t c = 0; c < nc; ++c) {
-                maxc = std::max(maxc, cnt[c + 1]);
-                cnt[c + 1] += cnt[c];
-            }
-            total = cnt[nc];
-            if (maxc > PT_GRID_MAX_CELL || total >= ((int64_t)1 << 31) - 1) return;
-            H->gcell.assign(cnt.begin(), cnt.end());
-            H->gref.assign((size_t)total, 0);
-        }
-    }
-    for (int a = 0; a < 3; ++a) {
-        K.g_org[a] = G0[a];
-        K.g_n[a] = n[a];
-    }
-    K.g_h = hf;
-    K.n_gref = (int32_t)total;
-    if (!H->bunitc.empty()) {
-        H->gunitc.resize((size_t)total);
-        for (int64_t i = 0; i < total; ++i) H->gunitc[i] = H->bunitc[H->gref[i]];
-    }
-}
-
-// Light-side cull of the uniform units' shadow tests (render loop,
-// pt_path.h).  A shadow ray from P toward a light point L is the line
-// P + s (L - P), |s| < 1 (main.py:37-47: two-sided, squared distance below
-// |L - P|^2).  Let h be a member triangle's signed plane distance (its
-// reference plane, utils.py:109-111).  If every corner of the light's box
-// has h > m1 (the light strictly on the positive side: so has every sampled
-// L, a point of the box) and h(P) > max h / 2 + m2, the line meets the plane at
-// s = h(P) / (h(P) - h(L)) with |s| - 1 >= min(m1 / h(P), 2 m2 / max h) > 0:
-// beyond L (h(L) < h(P)) or behind P farther than |L - P| (h(L) > h(P)),
-// certainly outside the reference's range for every light sample.  The
-// negative side is symmetric.  The kernel's f32 h(P) (origin_q, surface
-// frame) errs by at most U.eh from each member's h, so the thresholds
-// include eh and round outward:
-//   lc[0] = up(max h / 2 + m2 + eh)  (h > lc[0]: cull), +inf when no cull
-//   lc[1] = down(min h / 2 - m2 - eh) (h < lc[1]: cull), -inf when no cull
-// m1 = m2 = 1e-6 (relative margin >= ~1e-8 against the reference's own f64
-// rounding of t and of the squared distances, ~1e-11 even for grazing lines).
-inline void light_cull(HostScene* H, const pt_scene_desc* d) {
-    const int T = d->n_tri;
-    const double m1 = 1e-6, m2 = 1e-6;
-    H->unit_lc.assign(2 * (size_t)H->k.n_obj_unit, 0.f);
-    // the light's box: every sampled point lies in it (a convex combination
-    // of a light triangle's vertices), so h over its 8 corners bounds h over
-    // the light (cost independent of the light's triangle count)
-    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int lt = d->n_obj_tri; lt < T; ++lt)
-        for (int v = 0; v < 3; ++v) {
-            const D3 x = tri_vertex(d, lt, v);
-            const double xa[3] = {x.x, x.y, x.z};
-            for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], xa[a]); hi[a] = std::max(hi[a], xa[a]); }
-        }
-    for (int u = 0; u < H->k.n_obj_unit; ++u) {
-        const UnitF& U = H->unit[u];
-        float* lc = &H->unit_lc[2 * (size_t)u];
-        lc[0] = INFINITY;
-        lc[1] = -INFINITY;
-        if (!(U.eh >= 0.f) || !(U.eh < 1e30f) || !(lo[0] <= hi[0])) continue;   // degenerate / no light
-        double hmin = INFINITY, hmax = -INFINITY;
-        for (int m = 0; m < U.count; ++m) {
-            const TriD& E = H->trid[U.t[m]];
-            for (int c = 0; c < 8; ++c) {
-                const D3 x = d3((c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]);
-                const double h = E.vp[0] * x.x + E.vp[1] * x.y + E.vp[2] * x.z - E.cvp;
-                // + f64 rounding of h and of the sampled points (convex
-                // combinations rounded): far below 1e-9
-                const double e = 1e-9 * (1.0 + fabs(x.x) + fabs(x.y) + fabs(x.z) + fabs(E.cvp));
-                hmin = std::min(hmin, h - e);
-                hmax = std::max(hmax, h + e);
-            }
-        }
-        if (!(hmin <= hmax)) continue;
-        const double eh = (double)U.eh;
-        if (hmin > m1) lc[0] = f32_upb(hmax / 2 + m2 + eh);
-        else if (hmax < -m1) lc[1] = f32_down(hmin / 2 - m2 - eh);
-    }
 }
 
 // The 64-B form of the BVH units (UnitC, pt_core.h), when every unit is a
@@ -939,7 +755,6 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         acc += d->tri_area[t];
         H->light_cum.push_back(acc);
     }
-    light_cull(H, d);
     SceneK& K = H->k;
     K.n_tri = T;
     K.n_obj_tri = d->n_obj_tri;
@@ -959,7 +774,6 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     if (H->bunit.size() >= (size_t(1) << 24)) return "mesh too large: at most 2^24 BVH units";
     build_bvh(H, X);   // needs K.center and K.n_tri
     build_unitc(H);
-    build_grid(H, d, X);
     return "";
 }
 
@@ -979,10 +793,6 @@ inline void bind_host(HostScene* H) {
     H->k.mat = H->mat.data();
     H->k.light_tri = H->light_tri.data();
     H->k.light_cum = H->light_cum.data();
-    H->k.unit_lc = H->unit_lc.data();
-    H->k.gcell = H->gcell.empty() ? nullptr : H->gcell.data();
-    H->k.gref = H->gref.empty() ? nullptr : H->gref.data();
-    H->k.gunitc = H->gunitc.empty() ? nullptr : H->gunitc.data();
 }
 
 // first band row >= row_begin with iy % step == phase, and the band's row count

@@ -10,7 +10,26 @@ gather of the fixed-size row tiles to rank 0 assembles the framebuffer.
 
 The partition and assembly are pure functions so the CPU test suite can run
 them over gloo with world_size 2 (tests/test_distributed.py).
+
+Two ways to make the frame:
+  * device frame: each rank renders its band into a device tile, ONE gather
+    of the tiles to rank 0 (RCCL over xGMI with the nccl backend) and a
+    device assembly kernel put the frame in rank 0's HBM (gather_tiles,
+    assemble_bands_device) — for consumers on the GPU (the device image
+    finalisation, a PNG);
+  * host frame (HostFrame): the ranks of one node share a frame in
+    page-locked host memory (a /dev/shm mapping) and each GPU's render
+    writes its band straight into its rows, over its own PCIe link while the
+    kernel runs; a per-rank flag written after the render on its stream tells
+    rank 0 the frame is complete.  No gather and no separate device-to-host
+    copy: this is the frame SURVEY.md §8(d)'s metric asks for (kernel + D2H:
+    the framebuffer in host memory), at N GPUs as at one.
 """
+import ctypes as C
+import mmap
+import os
+import secrets
+
 import numpy as np
 
 
@@ -117,3 +136,124 @@ def render_distributed(renderer, width, height, spp=1, bounces=1, seed=None, rr=
     if return_tiles:
         return host
     return assemble(host, height)
+
+
+class HostFrame:
+    """A (height, width, 3) framebuffer ring in page-locked host memory shared
+    by the `world` rank processes of one node (/dev/shm/<name>), which each
+    GPU renders its interleaved band into directly (include/pt_capi.h: host
+    frames).  `slots` frames rotate so a rank can render step s + 1 while
+    rank 0 still reads step s; a rank waits before reusing a slot until rank 0
+    has released the step that last used it.
+
+    Layout: a 4096-B header — ready[r] (the last step + 1 rank r's band of
+    which is in the frame; written by the GPU, pt_signal) at byte 64 r,
+    released[slot] (the last step + 1 rank 0 is done with in that slot) at
+    byte 2048 + 64 slot — then the slots' frames.
+
+    Rank 0 creates the file (create=True) and hands its name to the others;
+    close() unmaps it and rank 0 removes it."""
+
+    HEADER = 4096
+    READY, RELEASED = 0, 2048
+
+    def __init__(self, height, width, world, rank, name, slots=2, dtype=np.float32, create=False):
+        from . import _native
+        if world > 32 or slots > 32:
+            raise ValueError("at most 32 ranks and 32 slots")
+        self.H, self.W, self.world, self.rank, self.slots = height, width, world, rank, slots
+        self.dtype = np.dtype(dtype)
+        self.frame_bytes = height * width * 3 * self.dtype.itemsize
+        self.bytes = self.HEADER + slots * self.frame_bytes
+        self.path = os.path.join("/dev/shm", name)
+        self.owner = create
+        flags = os.O_RDWR | (os.O_CREAT | os.O_EXCL if create else 0)
+        fd = os.open(self.path, flags, 0o600)
+        try:
+            if create:
+                os.ftruncate(fd, self.bytes)
+            self._mm = mmap.mmap(fd, self.bytes, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        self._cbuf = C.c_char.from_buffer(self._mm)
+        self.host = C.addressof(self._cbuf)
+        self._lib = _native.lib()
+        dev = C.c_void_p()
+        _native.check(self._lib.pt_host_map(C.c_void_p(self.host), self.bytes, C.byref(dev)),
+                      "pt_host_map")
+        self.dev = dev.value
+        self.u64 = np.frombuffer(self._mm, dtype=np.uint64, count=self.HEADER // 8)
+        self._iy_top = max(iy for iy in range(rank, height, world)) if rank < height else None
+
+    @staticmethod
+    def new_name():
+        return f"pt_frame_{os.getpid()}_{secrets.token_hex(4)}"
+
+    def frame(self, step):
+        """The frame of `step` (numpy view of the shared memory)."""
+        off = self.HEADER + (step % self.slots) * self.frame_bytes
+        return np.frombuffer(self._mm, dtype=self.dtype, count=self.H * self.W * 3,
+                             offset=off).reshape(self.H, self.W, 3)
+
+    def band_target(self, step):
+        """(device address, out_row_stride) of this rank's band in the frame of
+        `step`: its top row (iy_top, image row H-1-iy_top), every world-th row."""
+        if self._iy_top is None:
+            return None, 0
+        off = self.HEADER + (step % self.slots) * self.frame_bytes + \
+            (self.H - 1 - self._iy_top) * self.W * 3 * self.dtype.itemsize
+        return self.dev + off, self.world * self.W * 3
+
+    def render(self, renderer, p, step, stream, timeout_s=300.0):
+        """Enqueue this rank's band of `step` on `stream` (asynchronous): wait
+        (host) until the slot is released, render into the frame, then the
+        ready flag.  p: this rank's band params (row_step = world,
+        row_phase = rank, out_row_stride 0)."""
+        from . import _native
+        from ._abi import with_flags
+        need = step - self.slots + 1
+        if need > 0:
+            slot = step % self.slots
+            _native.check(self._lib.pt_wait_flags(
+                C.c_void_p(self.host + self.RELEASED + 64 * slot), 1, 8, need, timeout_s),
+                "pt_wait_flags (slot release)")
+        ptr, stride = self.band_target(step)
+        if ptr is not None:
+            renderer.render_device(with_flags(p, out_row_stride=stride), ptr, stream)
+        _native.check(self._lib.pt_signal(C.c_void_p(self.dev + self.READY + 64 * self.rank),
+                                          step + 1, C.c_void_p(stream or 0)), "pt_signal")
+
+    def wait(self, step, timeout_s=300.0):
+        """Host: until every rank's band of `step` is in the frame."""
+        from . import _native
+        _native.check(self._lib.pt_wait_flags(C.c_void_p(self.host + self.READY), self.world, 8,
+                                              step + 1, timeout_s), "pt_wait_flags (frame ready)")
+        return self.frame(step)
+
+    def release(self, step):
+        """Rank 0: done with the frame of `step` (its slot may be reused)."""
+        self.u64[(self.RELEASED + 64 * (step % self.slots)) // 8] = step + 1
+
+    def close(self):
+        if getattr(self, "_mm", None) is None:
+            return
+        from . import _native
+        _native.check(self._lib.pt_host_unmap(C.c_void_p(self.host)), "pt_host_unmap")
+        self.u64 = None
+        del self._cbuf
+        try:
+            self._mm.close()
+        except BufferError:   # a caller still holds a frame() view: unmapped with it
+            pass
+        self._mm = None
+        if self.owner:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

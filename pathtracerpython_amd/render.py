@@ -18,7 +18,6 @@ import numpy as np
 
 from . import _native
 from ._abi import (PT_FLAG_COUNT, PT_FLAG_FORCE_F64, PT_FLAG_KERNEL_TIMES, PT_FLAG_MEGAKERNEL,
-                   PT_FLAG_TREE_WALK,
                    PT_FLAG_OUT_F64, PT_FLAG_RR, PT_FLAG_WALK_COUNT, PtStats, band_rows, make_params)
 from .pack import pack_scene
 
@@ -48,13 +47,14 @@ class Renderer:
     def params(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
                rr_depth=3, force_f64=False, count=False, out_f64=False, row_begin=0,
                row_end=None, row_step=1, row_phase=0, sample_begin=0, megakernel=False,
-               walk_count=False, kernel_times=False, tree_walk=False):
+               walk_count=False, kernel_times=False, out_row_stride=0, lanes_per_pixel=0):
         """megakernel=True: scenes with a BVH render with the single kernel
         instead of the wavefront kernels (the same framebuffer, bit for bit).
         walk_count / kernel_times (wavefront renders): the walks' work counts /
-        per-kernel HIP-event times in the stats.  tree_walk=True: the
-        wavefront shadow walks go through the BVH even when the scene has a
-        grid (the same framebuffer, bit for bit)."""
+        per-kernel HIP-event times in the stats.  out_row_stride: elements
+        between output rows (0: packed).  lanes_per_pixel: 0 lets the
+        library choose per launch; a fixed power of two makes any band split
+        bit-identical (include/pt_capi.h)."""
         width = int(self.scene.width if width is None else width)
         height = int(self.scene.height if height is None else height)
         seed = self.scene.seed if seed is None else seed
@@ -62,10 +62,10 @@ class Renderer:
         flags = (PT_FLAG_RR if rr else 0) | (PT_FLAG_FORCE_F64 if force_f64 else 0) | \
             (PT_FLAG_COUNT if count else 0) | (PT_FLAG_OUT_F64 if out_f64 else 0) | \
             (PT_FLAG_MEGAKERNEL if megakernel else 0) | \
-            (PT_FLAG_WALK_COUNT if walk_count else 0) | (PT_FLAG_KERNEL_TIMES if kernel_times else 0) | \
-            (PT_FLAG_TREE_WALK if tree_walk else 0)
+            (PT_FLAG_WALK_COUNT if walk_count else 0) | (PT_FLAG_KERNEL_TIMES if kernel_times else 0)
         return make_params(width, height, spp, bounces, seed, flags, rr_depth, row_begin,
-                           row_end, row_step, row_phase, sample_begin)
+                           row_end, row_step, row_phase, sample_begin, out_row_stride,
+                           lanes_per_pixel)
 
     def band_rows(self, p):
         n = C.c_int32(0)
@@ -75,6 +75,8 @@ class Renderer:
     def render_params(self, p, stats=False):
         rows = self.band_rows(p)
         dt = np.float64 if p.flags & PT_FLAG_OUT_F64 else np.float32
+        if p.out_row_stride:
+            raise ValueError("render_params returns a packed band: use out_row_stride 0")
         out = np.zeros((rows, p.width, 3), dtype=dt)
         st = PtStats()
         _native.check(self._lib.pt_render(self._h, C.byref(p), C.c_void_p(out.ctypes.data),
@@ -181,9 +183,12 @@ def render(scene, width=None, height=None, spp=1, bounces=1, seed=None, rr=False
 class MultiRenderer:
     """One scene on several GPUs of this process (pt_render_multi): the rows
     are dealt out interleaved, every device renders its band concurrently and
-    each band is copied straight into its rows of the host framebuffer —
-    bit-identical to Renderer.render on one device.  (The multi-process path
-    over RCCL is distributed.py.)"""
+    each band is copied straight into its rows of the host framebuffer.
+    Bit-identical to Renderer.render on one device when both are given the
+    same lanes_per_pixel; with the default 0 each band's launch picks its own
+    lanes per pixel and the values agree to ~1e-15 relative (the sum order
+    of a pixel's samples follows its lane count).  (The multi-process path is
+    distributed.py.)"""
 
     def __init__(self, scene, devices):
         self.devices = [int(d) for d in devices]
@@ -195,10 +200,12 @@ class MultiRenderer:
         self.packed = first.packed
 
     def render(self, width=None, height=None, spp=1, bounces=1, seed=None, rr=False,
-               rr_depth=3, stats=False, out_f64=False, row_begin=0, row_end=None):
+               rr_depth=3, stats=False, out_f64=False, row_begin=0, row_end=None,
+               lanes_per_pixel=0):
         r0 = self.renderers[0]
         p = r0.params(width, height, spp, bounces, seed, rr, rr_depth, count=stats,
-                      out_f64=out_f64, row_begin=row_begin, row_end=row_end)
+                      out_f64=out_f64, row_begin=row_begin, row_end=row_end,
+                      lanes_per_pixel=lanes_per_pixel)
         rows = r0.band_rows(p)
         out = np.zeros((rows, p.width, 3), dtype=np.float64 if out_f64 else np.float32)
         hs = (C.c_void_p * len(self.renderers))(*[r._h.value for r in self.renderers])

@@ -100,19 +100,6 @@ int hc_render(const pt_scene_desc* d, const pt_render_params* p, int force64,
 // walks by QNode depth (root = 0)
 int hc_render_wavefront2(const pt_scene_desc* d, const pt_render_params* p, double* out,
                          int32_t* steps_out, int64_t* walk_stats, int64_t* depth_hist);
-// 1: hc_render_wavefront walks the shadow rays through the grid (build_grid)
-// instead of the tree; walk_stats then counts cells for node visits and
-// unit tests for leaf units
-static int g_hc_grid = 0;
-void hc_set_grid(int on) { g_hc_grid = on; }
-// grid shape: out[5] = {n_x, n_y, n_z, n_gref, built}
-int hc_grid_info(const pt_scene_desc* d, int32_t* out) {
-    HostScene H;
-    if (!prepare_scene(d, &H).empty()) return -1;
-    out[0] = H.k.g_n[0]; out[1] = H.k.g_n[1]; out[2] = H.k.g_n[2]; out[3] = H.k.n_gref;
-    out[4] = H.gcell.empty() ? 0 : 1;
-    return 0;
-}
 int hc_render_wavefront(const pt_scene_desc* d, const pt_render_params* p, double* out,
                         int32_t* steps_out, int64_t* walk_stats) {
     return hc_render_wavefront2(d, p, out, steps_out, walk_stats, nullptr);
@@ -187,27 +174,6 @@ int hc_render_wavefront2(const pt_scene_desc* d, const pt_render_params* p, doub
                 int ogrp;
                 wf_get_shadow1(SQ[i], k, &o32, &ogrp, &r);
                 ++ws[0];
-                if (g_hc_grid && H.k.gcell) {   // the grid walk, as k_wf_shadow_grid
-                    GridTrav G;
-                    const F3 inv = rcp_dir(r.d32);
-                    g_init(G, H.k, o32, r.d32, inv, r.hhi, shadow1_open(H.k, r));
-                    if (G.live) ++ws[1];
-                    while (G.live) {
-                        while (G.live && G.cur >= G.end) {
-                            G.live = g_next(G, H.k, o32, inv);
-                            if (G.live) ++ws[1];
-                        }
-                        if (!G.live) break;
-                        const int u = H.k.gref[G.cur++];
-                        if (g_mailbox(G, u)) continue;
-                        ++ws[3];
-                        if (H.k.bunitc) shadow1_unit(H.k, bvh_unit<true>(H.k, u), o32, ogrp, &r, sp);
-                        else shadow1_unit(H.k, bvh_unit<false>(H.k, u), o32, ogrp, &r, sp);
-                        if (!shadow1_open(H.k, r)) G.live = false;
-                    }
-                    wf_put_shadow1(&SQ[i], r);
-                    continue;
-                }
                 ShadowTrav1 T;
                 int buf[kBvhStackLocal];
                 const ShadowStack K{buf, 1};

@@ -211,15 +211,6 @@ int main(int argc, char** argv) {
             int64_t ws[8];
             CHECK(hc_render_wavefront(&S.d, &p, c.data(), &steps, ws) == 0);
             CHECK(a == c);   // wavefront == single kernel
-            // the grid shadow walks (build_grid, PT_GRID=1 in this build)
-            int32_t gi[5];
-            CHECK(hc_grid_info(&S.d, gi) == 0);
-            if (gi[4]) {
-                hc_set_grid(1);
-                CHECK(hc_render_wavefront(&S.d, &p, c.data(), &steps, ws) == 0);
-                hc_set_grid(0);
-                CHECK(a == c);   // grid walks == tree walks == single kernel
-            }
         }
         printf("scene %d: %d tris, bnodes %d depth %d qnodes %d, %llu tests\n", si, S.d.n_tri,
                info[0], info[1], info[2], (unsigned long long)(cnt[0] + cnt[1]));

@@ -45,7 +45,7 @@ def test_abi_struct_layout(hostcheck):
 
 def test_api_version():
     from pathtracerpython_amd._abi import PT_API_VERSION
-    assert _native.lib().pt_api_version() == PT_API_VERSION == 4
+    assert _native.lib().pt_api_version() == PT_API_VERSION == 5
 
 
 @pytest.mark.parametrize("H,step,phase,b,e", [(10, 1, 0, 0, 10), (10, 3, 1, 0, 10),
@@ -117,3 +117,42 @@ def test_image_without_gpu_fails_loudly():
     from pathtracerpython_amd.render import image_u8
     with pytest.raises(_native.NativeError, match="no HIP device"):
         image_u8(np.zeros((2, 2, 3)))
+
+
+def test_wait_flags_on_host():
+    """pt_wait_flags is host code (no GPU): all flags at or above the value
+    returns at once; a flag that never arrives times out with PT_ETIMEOUT."""
+    from pathtracerpython_amd._abi import PT_ETIMEOUT
+    lib = _native.lib()
+    f = np.zeros(16, dtype=np.uint64)
+    f[::4] = [3, 7, 3, 9]
+    ptr = C.c_void_p(f.ctypes.data)
+    assert lib.pt_wait_flags(ptr, 4, 4, 3, 1.0) == 0
+    assert lib.pt_wait_flags(ptr, 0, 4, 99, 0.0) == 0
+    assert lib.pt_wait_flags(ptr, 4, 4, 4, 0.05) == PT_ETIMEOUT
+    assert "flag 0" in _native.last_error()
+    assert lib.pt_wait_flags(ptr, 4, 0, 1, 0.05) == -1
+
+
+def test_render_params_validation_without_gpu():
+    """Flag bit 7 (v4's PT_FLAG_TREE_WALK) is retired, lanes_per_pixel must be
+    a power of two <= min(64, spp), out_row_stride 0 or >= width*3: rejected
+    by pt_render before any device is touched."""
+    lib = _native.lib()
+    out = np.zeros((4, 4, 3), dtype=np.float32)
+    for kw in (dict(flags=1 << 7), dict(lanes_per_pixel=3), dict(lanes_per_pixel=16),
+               dict(out_row_stride=11)):
+        p = make_params(4, 4, 8, 1, 0, **{k: v for k, v in kw.items() if k == "flags"})
+        for k, v in kw.items():
+            setattr(p, k, v)
+        assert lib.pt_render(None, C.byref(p), C.c_void_p(out.ctypes.data), None) == -1
+        assert "null scene" not in _native.last_error()
+
+
+def test_host_map_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    buf = np.zeros(4096, dtype=np.uint8)
+    dev = C.c_void_p()
+    assert _native.lib().pt_host_map(C.c_void_p(buf.ctypes.data), buf.nbytes, C.byref(dev)) == -4

@@ -330,10 +330,6 @@ def test_wavefront_k5_equals_single_kernel(k5small, W, spp, B, rr):
         # a band and a sample slice of the same image (kernel reuse, odd sizes)
         band = r.render(W, W, spp, B, 9, rr=rr, out_f64=True, row_begin=7, row_end=W - 3)
         assert np.array_equal(band, wf[3:W - 7])
-        # PT_FLAG_TREE_WALK: the shipped library builds no grid, so the
-        # shadow walks are the tree's either way (same frame)
-        tw = r.render_params(r.params(W, W, spp, B, 9, rr=rr, out_f64=True, tree_walk=True))
-        assert np.array_equal(tw, wf)
     rows = [0, W // 2, W - 1]
     pix = np.array([ix * W + iy for iy in rows for ix in range(0, W, 3)], dtype=np.int64)
     ref, _ = oracle.render(pk, W, W, spp, B, 9, flags=1 if rr else 0, pixels=pix)
@@ -529,3 +525,106 @@ def test_wavefront_walk_counts_and_times(k5small):
         assert np.array_equal(fb, ref)
         assert tt["shade_launches"] == tt["shadow_launches"] + 1 == tt["closest_launches"] + 1
         assert tt["shade_ms"] > 0 and tt["shadow_ms"] > 0 and tt["closest_ms"] > 0
+
+
+def test_render_multi_lanes_contract(cornell):
+    """at the K2 frame an 8-way split's bands run more lanes per
+    pixel than the whole frame (choose_split), so pt_render_multi with the
+    default lanes_per_pixel = 0 agrees with one render to rounding only;
+    with a fixed lanes_per_pixel both are the same bit for bit."""
+    from pathtracerpython_amd.render import MultiRenderer
+    W = H = 512
+    with Renderer(cornell) as r:
+        ref = r.render(W, H, 64, 4, 9, out_f64=True)
+        ref8 = r.render_params(r.params(W, H, 64, 4, 9, out_f64=True, lanes_per_pixel=8))
+        ref32 = r.render_params(r.params(W, H, 64, 4, 9, out_f64=True, lanes_per_pixel=32))
+    assert np.array_equal(ref8, ref)   # the whole K2 frame picks 8 lanes per pixel itself
+    with MultiRenderer(cornell, [0] * 8) as m:
+        auto = m.render(W, H, 64, 4, 9, out_f64=True)
+        assert np.abs(auto - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
+        assert np.array_equal(m.render(W, H, 64, 4, 9, out_f64=True, lanes_per_pixel=8), ref8)
+        assert np.array_equal(m.render(W, H, 64, 4, 9, out_f64=True, lanes_per_pixel=32), ref32)
+
+
+def test_render_multi_error_drains_launched_devices(cornell, monkeypatch):
+    """a failure while dealing band i (fault injected after
+    bands 0..i-1 were launched) returns the error after draining those
+    devices; the same handles then render bit-exactly."""
+    from pathtracerpython_amd.render import MultiRenderer
+    W = H = 256
+    with Renderer(cornell) as r:
+        ref = r.render_params(r.params(W, H, 64, 4, 5, lanes_per_pixel=16))
+    with MultiRenderer(cornell, [0] * 4) as m:
+        for i in (1, 3):
+            monkeypatch.setenv("PT_FAULT_INJECT_MULTI", str(i))
+            with pytest.raises(_native.NativeError, match=f"device {i}: fault injected"):
+                m.render(W, H, 64, 4, 5, lanes_per_pixel=16)
+            monkeypatch.delenv("PT_FAULT_INJECT_MULTI")
+            assert np.array_equal(m.render(W, H, 64, 4, 5, lanes_per_pixel=16), ref)
+
+
+def test_render_multi_rejects_mixed_scenes(cornell, tmp_path):
+    from pathtracerpython_amd.render import MultiRenderer
+    m = MultiRenderer(cornell, [0, 0])
+    try:
+        other = Renderer(quad_scene(tmp_path, 3))
+        m.renderers.append(other)
+        with pytest.raises(_native.NativeError, match="another scene"):
+            m.render(16, 16, 2, 2, 1)
+    finally:
+        m.close()
+
+
+def test_out_row_stride_writes_band_rows_into_a_frame(cornell):
+    """out_row_stride: each rank's interleaved band written straight into its
+    rows of one frame (device memory here) assembles the whole frame."""
+    import torch
+    W, H, world = 96, 61, 4
+    with Renderer(cornell) as r:
+        ref = r.render_params(r.params(W, H, 16, 3, 2, lanes_per_pixel=4))
+        frame = torch.full((H, W, 3), float("nan"), dtype=torch.float32, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        for rank in range(world):
+            iy_top = max(range(rank, H, world))
+            p = r.params(W, H, 16, 3, 2, row_step=world, row_phase=rank, lanes_per_pixel=4,
+                         out_row_stride=world * W * 3)
+            r.render_device(p, frame[H - 1 - iy_top].data_ptr(), s)
+        torch.cuda.synchronize()
+        assert np.array_equal(frame.cpu().numpy(), ref)
+        # pt_render's host copy honours the stride too
+        out = np.full((H, 2 * W, 3), -1.0, dtype=np.float32)
+        p = r.params(W, H, 16, 3, 2, lanes_per_pixel=4)
+        p.out_row_stride = 2 * W * 3
+        import ctypes as C
+        _native.check(_native.lib().pt_render(r._h, C.byref(p), C.c_void_p(out.ctypes.data), None),
+                      "pt_render")
+        assert np.array_equal(out[:, :W], ref) and (out[:, W:] == -1.0).all()
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_host_frame_bands_in_one_process(cornell, world):
+    """HostFrame (distributed.py): each rank's band rendered straight into
+    the page-locked shared frame, pt_signal / pt_wait_flags, slot rotation —
+    here every rank's handle in one process on device 0.  The frame equals
+    one render bit for bit (fixed lanes per pixel), step after step."""
+    from pathtracerpython_amd.distributed import HostFrame
+    import torch
+    W, H = 128, 77
+    s = torch.cuda.current_stream().cuda_stream
+    with Renderer(cornell) as r:
+        ref = r.render_params(r.params(W, H, 32, 4, 7, lanes_per_pixel=8))
+        name = HostFrame.new_name()
+        frames = [HostFrame(H, W, world, 0, name, create=True)]
+        frames += [HostFrame(H, W, world, k, name) for k in range(1, world)]
+        try:
+            for step in range(5):
+                for k, hf in enumerate(frames):
+                    p = r.params(W, H, 32, 4, 7, row_step=world, row_phase=k, lanes_per_pixel=8)
+                    hf.render(r, p, step, s, timeout_s=60)
+                got = frames[0].wait(step, timeout_s=60)
+                assert np.array_equal(got, ref), step
+                del got
+                frames[0].release(step)
+        finally:
+            for hf in frames[::-1]:
+                hf.close()

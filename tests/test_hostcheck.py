@@ -245,38 +245,6 @@ def test_wavefront_equals_single_kernel_small_k5(hostcheck, tmp_path):
     _wavefront_case(hostcheck, pk, 8, 8, 1, 1, 3)                 # primary shading only
 
 
-@pytest.mark.parametrize("kind", ["k5", "random"])
-def test_grid_shadow_walk_equals_tree_walk(hostcheck, tmp_path, kind):
-    """The grid shadow walks (pt_prepare.h build_grid, pt_path.h grid shadow
-    walks; built in the host check only) give the tree walks'
-    framebuffer bit for bit, with the single kernel's."""
-    from pathtracerpython_amd import scene_reader
-    from pathtracerpython_amd.synth import write_k5_scene
-    scene_reader.VERBOSE = False
-    if kind == "k5":
-        pk = pack_scene(scene_reader.Scene(write_k5_scene(str(tmp_path), n_tris=4000, seed=3, size=16)))
-    else:
-        pk = pack_scene(random_scene(tmp_path, 1500, 7))
-    info = (C.c_int32 * 5)()
-    assert hostcheck.hc_grid_info(C.byref(pk.desc), info) == 0
-    assert info[4] == 1 and info[3] > 0
-    outs = []
-    for grid in (0, 1):
-        hostcheck.hc_set_grid(grid)
-        try:
-            outs.append(_wavefront_case(hostcheck, pk, 14, 14, 2, 4, 5))
-        finally:
-            hostcheck.hc_set_grid(0)
-    assert np.array_equal(outs[0], outs[1])
-
-
-def test_no_grid_without_mesh(hostcheck, cornell):
-    """Scenes without a BVH get no grid (build_grid runs on BVH units only)."""
-    info = (C.c_int32 * 5)()
-    assert hostcheck.hc_grid_info(C.byref(pack_scene(cornell).desc), info) == 0
-    assert list(info) == [0, 0, 0, 0, 0]
-
-
 def test_mesh_golden_bvh_and_wavefront(hostcheck, mesh_golden):
     """The host build's BVH walks (forced f64 and hybrid) and its wavefront
     state machine on the edge-case mesh scene, against the reference's render
