@@ -3,12 +3,24 @@
 
 One step = one render of a fixed frame (the whole main.py:186-280 loop:
 every pixel, every sample, every bounce, the /spp average) with the scene
-resident in HBM, plus — inside the timed step — the RCCL gather of the row
-bands to rank 0 (N > 1) and their device-side assembly: the step ends
-with the whole framebuffer in rank 0's HBM.  The framebuffer's PCIe copy to
-pinned host memory is timed separately after the timed region and reported
-beside `value` (d2h_ms, value_with_d2h): the PCIe-inclusive rate is never
-`value`.
+resident in HBM, ending with the framebuffer in HOST memory — SURVEY.md
+§8(d)'s metric is N_ps / render wall-time including the kernel and the D2H.
+Two frame transports (--frame):
+  host (default)  every rank's render writes its band straight into its rows
+                  of one page-locked frame in /dev/shm shared by the ranks of
+                  the node (distributed.HostFrame): the framebuffer crosses
+                  PCIe while the kernel runs, each GPU over its own link; a
+                  per-rank flag written on the render's stream (pt_signal)
+                  tells rank 0 the frame is complete (pt_wait_flags).  Frames
+                  rotate over 2 slots, so the next step's render is queued
+                  before rank 0 waits for this one.
+  device          each rank renders into a device tile; N > 1: ONE gather of
+                  the tiles to rank 0 (RCCL over xGMI) and the device band
+                  assembly (pt_assemble_bands_device); then rank 0's PCIe copy
+                  of the frame to pinned host memory.
+The other transport is measured after the headline one with the same steps
+and reported under `frame_modes`, with per-leg times (max / min band kernel
+over ranks; device: gather, assembly, D2H on rank 0's stream).
 
 Workloads (--config, BASELINE.json configs):
   k2 (default)  Cornell 512x512, 64 spp, 4 bounces (configs[1], the config the
@@ -32,17 +44,18 @@ Printed on rank 0: one JSON line with the driver's fields plus
                  k2/k4: k_render, FP32 VALU: reference-semantics ray-triangle
                  tests (exact, from a counting launch) x 47 FLOP (SURVEY.md
                  §8d) / HIP-event kernel time, vs 157.3 TF/s.  k5: the BVH
-                 walk kernels (shadow and closest), L2 roof: algorithmic
-                 bytes (node + leaf records + query records, from a counting
-                 launch) / their HIP-event time.  traffic: rocprofv3 PMC
-                 bytes per launch from profiles/, only when measured on the
+                 walk kernel with the larger own time (a profiling launch
+                 that runs the two walks one after the other), L2 roof:
+                 algorithmic bytes (node + leaf records + query records, from
+                 a counting launch) / its HIP-event time.  traffic: rocprofv3
+                 PMC bytes per launch from profiles/, only when measured on the
                  current kernel sources (tests/test_profiles.py).
   cpu_baseline : the C oracle (f64 restatement of the reference loop, test
                  infrastructure) on this host's CPU share, on a bounded sample
-  linf_vs_cpu_ref : per-pixel L-inf of this run's f32 framebuffer (as timed)
-                 vs the oracle — k2: every pixel of the frame (the oracle
-                 frame the cpu_baseline leg renders), with the counts of
-                 pixels above 1e-6 and 1e-4; k4/k5: a pixel sample
+  linf_vs_cpu_ref : per-pixel L-inf of this run's f32 framebuffer (as timed,
+                 read from host memory) vs the oracle — k2: every pixel of the
+                 frame (the oracle frame the cpu_baseline leg renders), with
+                 the counts of pixels above 1e-6 and 1e-4; k4/k5: a pixel sample
 """
 import argparse
 import hashlib
@@ -93,6 +106,8 @@ def parse():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="k2")
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
     ap.add_argument("--spp", type=int, default=None, help="override spp (k4)")
+    ap.add_argument("--frame", choices=("host", "device"), default="host",
+                    help="how the framebuffer reaches host memory (module docstring)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip L-inf vs the CPU oracle")
     a = ap.parse_args()
@@ -137,6 +152,109 @@ def load_traffic(config):
     return d.get("hbm_bytes_per_launch"), d.get("source")
 
 
+def rank_legs(vals, dist, world, device):
+    """(max, min) over ranks of this rank's value."""
+    if world == 1:
+        return vals, vals
+    import torch
+    t = torch.tensor([vals, -vals], dtype=torch.float64,
+                     device=device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]), float(-t[1])
+
+
+def run_host_frame(ctx, steps, warmup, base):
+    """The host-frame transport: returns (elapsed s over `steps` steps, rank
+    0's render-launch ms per step, the frame of the last step on rank 0 or
+    None, the next free step number)."""
+    import torch
+    r, p, hf, stream, rank, world, dist = (ctx[k] for k in ("r", "p", "hf", "stream", "rank", "world",
+                                                            "dist"))
+
+    def loop(first, n, evs=None):
+        ev = (lambda i: evs[i]) if evs else (lambda i: None)
+        if rank == 0:
+            hf.render(r, p, first, stream, events=ev(0))
+            for i in range(n):
+                if i + 1 < n:
+                    hf.render(r, p, first + i + 1, stream, events=ev(i + 1))
+                hf.wait(first + i)
+                hf.release(first + i)
+        else:
+            for i in range(n):
+                hf.render(r, p, first + i, stream, events=ev(i))
+
+    loop(base, warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    t0 = time.perf_counter()
+    loop(base + warmup, steps, evs)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    last = base + warmup + steps - 1
+    fb = hf.frame(last).copy() if rank == 0 else None
+    return elapsed, [a.elapsed_time(b) for a, b in evs], fb, last + 1
+
+
+def run_device_frame(ctx, steps, warmup):
+    """The device-frame transport: render into a device tile, N > 1: RCCL
+    gather + device assembly on rank 0, then rank 0's D2H copy to pinned host
+    memory.  Returns (elapsed s, rank 0's per-step leg ms {render, gather,
+    assembly, d2h}, the last frame on rank 0 or None)."""
+    import torch
+    from pathtracerpython_amd.distributed import assemble_bands_device
+    r, p, stream, rank, world, dist = (ctx[k] for k in ("r", "p", "stream", "rank", "world", "dist"))
+    H, W, max_rows = ctx["H"], ctx["W"], ctx["max_rows"]
+    tile = torch.zeros((max_rows, W, 3), dtype=torch.float32, device="cuda")
+    host = gathered = frame = None
+    if rank == 0:
+        host = torch.empty((H, W, 3), dtype=torch.float32).pin_memory()
+        if world > 1:
+            gathered = torch.empty((world, max_rows, W, 3), dtype=torch.float32, device="cuda")
+            frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+        else:
+            frame = tile
+
+    def step(ev=None):
+        rec = (lambda k: ev[k].record()) if ev else (lambda k: None)
+        rec(0)
+        r.render_device(p, tile.data_ptr(), stream.cuda_stream)
+        rec(1)
+        if world > 1:
+            dist.gather(tile, gather_list=list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+        rec(2)
+        if rank == 0:
+            if world > 1:
+                assemble_bands_device(gathered, frame, stream.cuda_stream)
+            rec(3)
+            host.copy_(frame[:H], non_blocking=True)
+        rec(4)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    legs = {k: [e[j].elapsed_time(e[j + 1]) for e in evs]
+            for j, k in enumerate(("render", "gather", "assembly", "d2h"))}
+    return elapsed, legs, (host.numpy().copy() if rank == 0 else None)
+
+
 def main():
     args = parse()
     from pathtracerpython_amd.launch import pg_timeout, rank_env, spawn_ranks, under_launcher
@@ -149,13 +267,24 @@ def main():
     rank, local, world = rank_env()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # PT_BENCH_REHEARSE=1 (tests only): every rank on device 0 over gloo, the
+    # host-frame transport alone — the N > 1 code path on a one-GPU box (its
+    # timings mean nothing: the ranks share the GPU)
+    rehearse = os.environ.get("PT_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
+        args.frame = "host"
     torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout())
+        if rehearse:
+            dist.init_process_group("gloo", timeout=pg_timeout())
+        else:
+            dist.init_process_group("nccl", device_id=device, timeout=pg_timeout())
 
     from oracle.oracle import host_threads
     from pathtracerpython_amd import scene_reader
-    from pathtracerpython_amd.distributed import assemble_bands_device, band_rows_of
+    from pathtracerpython_amd.distributed import HostFrame, band_rows_of
     from pathtracerpython_amd.render import Renderer
     scene_reader.VERBOSE = False
     cfg = dict(CONFIGS[args.config])
@@ -164,86 +293,83 @@ def main():
     W, H, SPP, B = cfg["W"], cfg["H"], cfg["spp"], cfg["bounces"]
     if args.scaling == "weak":
         H = cfg["H"] * world
+
+    def bcast(obj):   # rank 0's object to every rank
+        if world == 1:
+            return obj
+        o = [obj]
+        dist.broadcast_object_list(o, src=0)
+        return o[0]
+
     if args.config == "k5":
         from pathtracerpython_amd.synth import write_k5_scene
         tmp = tempfile.mkdtemp(prefix="k5_")
-        sdl = write_k5_scene(tmp, n_tris=100_000, seed=0, size=W) if rank == 0 else None
-        if world > 1:   # one writer, every rank reads the same files
-            obj = [sdl]
-            dist.broadcast_object_list(obj, src=0)
-            sdl = obj[0]
-        scene = scene_reader.Scene(sdl)
+        sdl = bcast(write_k5_scene(tmp, n_tris=100_000, seed=0, size=W) if rank == 0 else None)
+        scene = scene_reader.Scene(sdl)   # one writer, every rank reads the same files
     else:
         scene = scene_reader.Scene(os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl"))
     r = Renderer(scene)
     p = r.params(W, H, SPP, B, SEED, row_begin=0, row_end=H, row_step=world, row_phase=rank)
     rows = r.band_rows(p)
-    max_rows = (H + world - 1) // world
     assert rows == len(band_rows_of(H, rank, world))
     stream = torch.cuda.current_stream()
-    tile = torch.zeros((max_rows, W, 3), dtype=torch.float32, device="cuda")
-    if rank == 0:
-        host = torch.empty((H, W, 3), dtype=torch.float32).pin_memory()
-        if world > 1:
-            gathered = torch.empty((world, max_rows, W, 3), dtype=torch.float32, device="cuda")
-            frame = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
-        else:
-            frame = tile
-
-    def step(ev=None):
-        if ev:
-            ev[0].record(stream)
-        r.render_device(p, tile.data_ptr(), stream.cuda_stream)
-        if ev:
-            ev[1].record(stream)
-        if world > 1:
-            dist.gather(tile, gather_list=list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                assemble_bands_device(gathered, frame, stream.cuda_stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+    name = bcast(HostFrame.new_name() if rank == 0 else None)
+    if world > 1:
+        dist.barrier()   # rank 0 creates the file first
+    hf = HostFrame(H, W, world, rank, name, create=(rank == 0)) if rank == 0 else None
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    # HIP events around every render launch, on the stream it is launched on
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    render_ms = [a.elapsed_time(b) for a, b in evs]
-    ms_per_step = elapsed / args.steps * 1e3
+        if rank != 0:
+            hf = HostFrame(H, W, world, rank, name)
+    ctx = dict(r=r, p=p, hf=hf, stream=stream.cuda_stream, rank=rank, world=world, dist=dist,
+               H=H, W=W, max_rows=(H + world - 1) // world)
     paths = W * H * SPP
-    value = paths / (elapsed / args.steps) / 1e6
+
+    def host_mode(base):
+        el, ks, fb, nxt = run_host_frame(ctx, args.steps, args.warmup, base)
+        el, _ = rank_legs(el, dist, world, device)
+        km = float(np.mean(ks))
+        kmax, kmin = rank_legs(km, dist, world, device)
+        ms = el / args.steps * 1e3
+        return {"ms_per_step": round(ms, 4), "value": round(paths / (ms * 1e-3) / 1e6, 2),
+                "legs_ms": {"band_kernel_max": round(kmax, 4), "band_kernel_min": round(kmin, 4),
+                            "after_kernel": round(ms - kmax, 4)},
+                "_k_ms": km, "_fb": fb, "_next": nxt}
+
+    def device_mode():
+        dctx = dict(ctx, stream=stream)
+        el, legs, fb = run_device_frame(dctx, args.steps, args.warmup)
+        el, _ = rank_legs(el, dist, world, device)
+        km = float(np.mean(legs["render"]))
+        kmax, kmin = rank_legs(km, dist, world, device)
+        ms = el / args.steps * 1e3
+        lg = {"band_kernel_max": round(kmax, 4), "band_kernel_min": round(kmin, 4)}
+        if rank == 0:
+            for k in ("gather", "assembly", "d2h"):
+                lg[k] = round(float(np.mean(legs[k])), 4)
+        return {"ms_per_step": round(ms, 4), "value": round(paths / (ms * 1e-3) / 1e6, 2),
+                "legs_ms": lg, "_k_ms": km, "_fb": fb}
+
+    if args.frame == "host":
+        head = host_mode(0)
+        other = {"skipped": "PT_BENCH_REHEARSE (gloo cannot gather device tensors)", "_fb": None} \
+            if rehearse else device_mode()
+    else:
+        head = device_mode()
+        other = host_mode(0)
+    modes = {args.frame: head, ("device" if args.frame == "host" else "host"): other}
+    k_ms = head["_k_ms"]
+    fb = head["_fb"]
+    ms_per_step = head["ms_per_step"]
+    value = head["value"]
 
     result = None
     if rank == 0:
         from oracle import oracle
-        # the framebuffer's PCIe leg, outside the timed region: the D2H copy
-        # to pinned host memory (median of 10)
-        d2h = []
-        for _ in range(10):
-            t1 = time.perf_counter()
-            host.copy_(frame[:H])
-            torch.cuda.synchronize()
-            d2h.append((time.perf_counter() - t1) * 1e3)
-        d2h_ms = float(np.median(d2h))
-        k_ms = float(np.mean(render_ms))
         if args.config == "k5":
             roofline = k5_roofline(r, p, k_ms)
         else:
             roofline = k_render_roofline(r, p, k_ms, W, rows, SPP, args.config)
-        fb = host.numpy()
         linf = checked = over = None
         cpu = None
         want_cpu = not args.no_cpu_baseline and world == 1
@@ -263,6 +389,10 @@ def main():
                 linf = float(err.max())
                 checked = f"all {W * H} pixels"
                 over = {"1e-6": int((err > 1e-6).sum()), "1e-4": int((err > 1e-4).sum())}
+                # the other transport's frame: the same pixels to the bit
+                # when both ran the same launches
+                if other["_fb"] is not None:
+                    modes["frames_bitwise_equal"] = bool(np.array_equal(other["_fb"], fb))
         else:
             if not args.no_check:
                 if args.config == "k5":
@@ -281,29 +411,38 @@ def main():
                 over = {"1e-6": int((err > 1e-6).sum()), "1e-4": int((err > 1e-4).sum())}
             if want_cpu:
                 cpu = cpu_baseline(oracle, r.packed, W, H, SPP, B, args.config)
-        parallel = f"rows interleaved over {world} GPU" + ("s + RCCL gather" if world > 1 else "")
+        parallel = f"rows interleaved over {world} GPU" + ("s" if world > 1 else "") + \
+            (", bands written into one shared page-locked host frame" if args.frame == "host" else
+             (" + RCCL gather + device assembly" if world > 1 else "") + " + D2H copy")
         wl = cfg["workload"].format(spp=SPP)
         if args.scaling == "weak":
-            wl = f"Cornell box 512 x (512 N) 64 spp 4 bounces, 512 rows per GPU (weak scaling)"
+            wl = "Cornell box 512 x (512 N) 64 spp 4 bounces, 512 rows per GPU (weak scaling)"
+        for m in modes.values():
+            if isinstance(m, dict):
+                for k in [k for k in m if k.startswith("_")]:
+                    del m[k]
         result = {
             "metric": METRIC,
-            "value": round(value, 2), "unit": "Mpath-samples/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "value": value, "unit": "Mpath-samples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": "f32+f64", "data": "synthetic",
             "config": {"workload": wl, "width": W, "height": H, "spp": SPP, "bounces": B,
-                       "seed": SEED, "parallelism": parallel,
-                       "timed_step": "render + (RCCL gather + device band assembly): "
-                                     "the framebuffer resident in rank 0's HBM"},
-            "d2h_ms": round(d2h_ms, 4),
-            "value_with_d2h": round(paths / ((ms_per_step + d2h_ms) * 1e-3) / 1e6, 2),
-            "d2h_note": "PCIe copy of the f32 framebuffer to pinned host memory, timed "
-                        "after the timed region (not part of value)",
+                       "seed": SEED, "parallelism": parallel, "frame": args.frame,
+                       "timed_step": "render + the framebuffer in host memory (SURVEY.md §8(d): "
+                                     "kernel + D2H), " +
+                                     ("each GPU writing its band into one shared page-locked frame"
+                                      if args.frame == "host" else
+                                      "RCCL gather + device assembly (N > 1) + D2H copy")},
+            "frame_modes": modes,
             "linf_vs_cpu_ref": linf, "linf_checked": checked, "pixels_over": over,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+    hf.close()
     r.close()
     if world > 1:
         dist.barrier()
@@ -314,10 +453,8 @@ def main():
 def k_render_roofline(r, p, k_ms, W, rows, SPP, config):
     """k_render against the FP32 VALU roof: exact reference-semantics test
     count of this rank's launch (separate counting launch) x 47 FLOP."""
-    from pathtracerpython_amd._abi import PT_FLAG_COUNT, make_params
-    pc = make_params(p.width, p.height, p.spp, p.bounces, p.seed, p.flags | PT_FLAG_COUNT,
-                     p.rr_depth, p.row_begin, p.row_end, p.row_step, p.row_phase, p.sample_begin)
-    _, st = r.render_params(pc, stats=True)
+    from pathtracerpython_amd._abi import PT_FLAG_COUNT, with_flags
+    _, st = r.render_params(with_flags(p, PT_FLAG_COUNT, out_row_stride=0), stats=True)
     tests = st["closest_tests"] + st["shadow_tests"]
     achieved = tests * FLOP_PER_TEST / (k_ms * 1e-3) / 1e12
     traffic, tsrc = load_traffic(config)
@@ -339,21 +476,20 @@ def k_render_roofline(r, p, k_ms, W, rows, SPP, config):
 
 def k5_roofline(r, p, render_ms):
     """The wavefront render's two walk kernels (k_wf_shadow, k_wf_closest):
-    algorithmic bytes of their launches (counting launch) over their
-    HIP-event time (a profiling launch of the production kernels), against
-    the L2 roof — the BVH (9.6 MB of nodes and leaf records) is served from
-    the XCDs' L2 (~92% hit) and the rate of its record reads exceeds HBM's
-    peak; the PMC traffic beyond L2 is reported beside it as hbm_frac.  The
-    top-level object is the walk with the larger HIP-event time per render
-    (the two overlap on two streams: a walk's time includes the stretches it
-    waits for CUs the other one holds), the other one is `other_walk`."""
-    from pathtracerpython_amd._abi import PT_FLAG_KERNEL_TIMES, PT_FLAG_WALK_COUNT, make_params
-
-    def with_flags(f):
-        return make_params(p.width, p.height, p.spp, p.bounces, p.seed, p.flags | f, p.rr_depth,
-                           p.row_begin, p.row_end, p.row_step, p.row_phase, p.sample_begin)
-    _, wc = r.render_params(with_flags(PT_FLAG_WALK_COUNT), stats=True)
-    _, kt = r.render_params(with_flags(PT_FLAG_KERNEL_TIMES), stats=True)
+    algorithmic bytes of their launches (counting launch) over their own
+    HIP-event time (a PT_FLAG_KERNEL_TIMES launch of the production kernels,
+    which runs the two walks of a step one after the other on one stream, so
+    neither time includes waiting for CUs the other holds), against the L2
+    roof — the BVH (9.6 MB of nodes and leaf records) is served from the
+    XCDs' L2 (~92% hit) and the rate of its record reads exceeds HBM's peak.
+    The top-level object is the walk with the larger own time per render, the
+    other one is `other_walk`.  `traffic` is the PMC bytes the walk moves
+    beyond L2 (TCC FETCH_SIZE + WRITE_SIZE: Infinity Cache hits included, so
+    an upper bound of its HBM bytes), reported against HBM's peak as
+    beyond_l2_frac."""
+    from pathtracerpython_amd._abi import PT_FLAG_KERNEL_TIMES, PT_FLAG_WALK_COUNT, with_flags
+    _, wc = r.render_params(with_flags(p, PT_FLAG_WALK_COUNT, out_row_stride=0), stats=True)
+    _, kt = r.render_params(with_flags(p, PT_FLAG_KERNEL_TIMES, out_row_stride=0), stats=True)
     traffic = load_traffic_record("k5")
 
     def walk(kind):
@@ -369,9 +505,11 @@ def k5_roofline(r, p, render_ms):
             tr = traffic.get("hbm_bytes_per_launch" if kind == "shadow" else "closest_hbm_bytes_per_launch")
         return {"bound": "l2", "achieved": round(achieved, 2), "peak": L2_GATHER_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / L2_GATHER_PEAK_GBS, 4), "traffic": tr,
+                "traffic_level": "beyond L2 (TCC FETCH_SIZE + WRITE_SIZE, FETCH doubled for gfx950; "
+                                 "Infinity Cache hits included: an upper bound of HBM bytes)",
                 "kernel": f"k_wf_{kind}<true,false> (persistent " +
                           ("one-ray shadow walks)" if kind == "shadow" else "closest-hit walks)"),
-                "hbm_frac": (round(tr / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None),
+                "beyond_l2_frac": (round(tr / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tr else None),
                 "work_per_launch": {"queries": wc[f"{kind}_queries"] / nl,
                                     "node_visits": wc[f"{kind}_node_visits"] / nl,
                                     "leaf_unit_tests": wc[f"{kind}_leaf_units"] / nl,
@@ -380,18 +518,21 @@ def k5_roofline(r, p, render_ms):
                                                    f"per leaf unit + {q_b} B per query (its record "
                                                    f"read, list entry, result written)"},
                 "kernel_ms_mean": round(launch_ms, 4), "launches_per_render": nl,
-                "kernel_ms_per_render": round(kt[f"{kind}_ms"], 2)}
+                "kernel_ms_per_render": round(kt[f"{kind}_ms"], 2),
+                "time_basis": "own time: the walks of a step run one after the other in this "
+                              "profiling launch (PT_FLAG_KERNEL_TIMES)"}
     sh, cl = walk("shadow"), walk("closest")
     top, other = (sh, cl) if kt["shadow_ms"] >= kt["closest_ms"] else (cl, sh)
     top = dict(top)
     top.update({"note": "latency-bound pointer chasing over an L2-resident BVH: the peak is the "
                         "L2-served gather rate of MI355X_MICROARCH.md (16.8-18.8 TB/s); the record "
-                        "reads run above HBM's 8 TB/s, the PMC bytes beyond L2 are traffic / hbm_frac",
+                        "reads run above HBM's 8 TB/s, the PMC bytes beyond L2 are traffic / "
+                        "beyond_l2_frac",
                 "other_walk": other,
                 "render_ms_mean": round(render_ms, 3),
-                "kernel_ms_per_render_all": {"shade": round(kt["shade_ms"], 2),
-                                             "shadow": round(kt["shadow_ms"], 2),
-                                             "closest": round(kt["closest_ms"], 2)},
+                "kernel_ms_per_render_serial": {"shade": round(kt["shade_ms"], 2),
+                                                "shadow": round(kt["shadow_ms"], 2),
+                                                "closest": round(kt["closest_ms"], 2)},
                 "traffic_source": traffic.get("source") if traffic else
                 load_traffic("k5")[1], "kernel_source_sha": source_sha()})
     return top

@@ -57,7 +57,9 @@ extern "C" {
                                           leaf-unit tests into pt_stats
                                           (counting kernels; synchronous)  */
 #define PT_FLAG_KERNEL_TIMES (1u << 6) /* wavefront renders: per-kernel HIP-event
-                                          times into pt_stats (synchronous) */
+                                          times into pt_stats (synchronous; the
+                                          two walks of a step run one after the
+                                          other, so each time is its own)   */
 /* bit 7: reserved (v4's PT_FLAG_TREE_WALK, retired in v5 with the grid-walk
    experiment it selected against; the library rejects it)                */
 #define PT_FLAG_RESERVED7 (1u << 7)

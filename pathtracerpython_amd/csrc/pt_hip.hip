@@ -1121,19 +1121,23 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
         if (step + 1 < steps) {
             // the two walks only read the shade step's output and write
             // disjoint records: the closest walks run on a side stream
-            hipStream_t cs = PT_WF_CONCURRENT ? s->wf_side : st;
-            if (PT_WF_CONCURRENT) {
+            // (PT_FLAG_KERNEL_TIMES launches run them one after the other on
+            // one stream, so each walk's HIP-event time is its own time on
+            // the whole chip, not the stretches it waits for the other's CUs)
+            const bool side = PT_WF_CONCURRENT && !times;
+            hipStream_t cs = side ? s->wf_side : st;
+            if (side) {
                 HIPCHK(hipEventRecord(s->wf_ev_shade, st));
                 HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
             }
             HIPCHK(mark(step, 2, 0, cs));
             closest_walk(cs, step);
             HIPCHK(mark(step, 2, 1, cs));
-            if (PT_WF_CONCURRENT) HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
+            if (side) HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
             HIPCHK(mark(step, 1, 0, st));
             shadow_walk(st);
             HIPCHK(mark(step, 1, 1, st));
-            if (PT_WF_CONCURRENT) HIPCHK(hipStreamWaitEvent(st, s->wf_ev_walk, 0));
+            if (side) HIPCHK(hipStreamWaitEvent(st, s->wf_ev_walk, 0));
         }
     }
     hipLaunchKernelGGL(k_wf_final, grid, dim3(256), 0, st, s->dev, R, (const WfPath*)W, out_dev);

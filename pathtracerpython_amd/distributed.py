@@ -157,7 +157,10 @@ class HostFrame:
     HEADER = 4096
     READY, RELEASED = 0, 2048
 
-    def __init__(self, height, width, world, rank, name, slots=2, dtype=np.float32, create=False):
+    def __init__(self, height, width, world, rank, name, slots=2, dtype=np.float32, create=False,
+                 map_device=True):
+        """map_device=False: the shared memory and its flags only, no HIP
+        mapping (no render(); the CPU tests of the protocol use it)."""
         from . import _native
         if world > 32 or slots > 32:
             raise ValueError("at most 32 ranks and 32 slots")
@@ -178,12 +181,18 @@ class HostFrame:
         self._cbuf = C.c_char.from_buffer(self._mm)
         self.host = C.addressof(self._cbuf)
         self._lib = _native.lib()
-        dev = C.c_void_p()
-        _native.check(self._lib.pt_host_map(C.c_void_p(self.host), self.bytes, C.byref(dev)),
-                      "pt_host_map")
-        self.dev = dev.value
+        self.dev = None
+        if map_device:
+            dev = C.c_void_p()
+            rc = self._lib.pt_host_map(C.c_void_p(self.host), self.bytes, C.byref(dev))
+            if rc != 0:
+                err = _native.last_error()
+                self.close()
+                raise _native.NativeError(f"pt_host_map failed ({rc}): {err}")
+            self.dev = dev.value
         self.u64 = np.frombuffer(self._mm, dtype=np.uint64, count=self.HEADER // 8)
         self._iy_top = max(iy for iy in range(rank, height, world)) if rank < height else None
+        self.band_rows = list(range(rank, height, world))[::-1]   # iy, top row first
 
     @staticmethod
     def new_name():
@@ -198,17 +207,18 @@ class HostFrame:
     def band_target(self, step):
         """(device address, out_row_stride) of this rank's band in the frame of
         `step`: its top row (iy_top, image row H-1-iy_top), every world-th row."""
-        if self._iy_top is None:
+        if self._iy_top is None or self.dev is None:
             return None, 0
         off = self.HEADER + (step % self.slots) * self.frame_bytes + \
             (self.H - 1 - self._iy_top) * self.W * 3 * self.dtype.itemsize
         return self.dev + off, self.world * self.W * 3
 
-    def render(self, renderer, p, step, stream, timeout_s=300.0):
+    def render(self, renderer, p, step, stream, timeout_s=300.0, events=None):
         """Enqueue this rank's band of `step` on `stream` (asynchronous): wait
         (host) until the slot is released, render into the frame, then the
         ready flag.  p: this rank's band params (row_step = world,
-        row_phase = rank, out_row_stride 0)."""
+        row_phase = rank, out_row_stride 0).  events: optional (start, end)
+        torch.cuda.Events recorded around the render launch."""
         from . import _native
         from ._abi import with_flags
         need = step - self.slots + 1
@@ -217,9 +227,15 @@ class HostFrame:
             _native.check(self._lib.pt_wait_flags(
                 C.c_void_p(self.host + self.RELEASED + 64 * slot), 1, 8, need, timeout_s),
                 "pt_wait_flags (slot release)")
+        if self.dev is None:
+            raise ValueError("HostFrame opened with map_device=False: no device renders")
         ptr, stride = self.band_target(step)
+        if events:
+            events[0].record()
         if ptr is not None:
             renderer.render_device(with_flags(p, out_row_stride=stride), ptr, stream)
+        if events:
+            events[1].record()
         _native.check(self._lib.pt_signal(C.c_void_p(self.dev + self.READY + 64 * self.rank),
                                           step + 1, C.c_void_p(stream or 0)), "pt_signal")
 
@@ -238,7 +254,9 @@ class HostFrame:
         if getattr(self, "_mm", None) is None:
             return
         from . import _native
-        _native.check(self._lib.pt_host_unmap(C.c_void_p(self.host)), "pt_host_unmap")
+        if self.dev is not None:
+            self.dev = None
+            _native.check(self._lib.pt_host_unmap(C.c_void_p(self.host)), "pt_host_unmap")
         self.u64 = None
         del self._cbuf
         try:

@@ -1,0 +1,83 @@
+"""One rank of the HostFrame tests (started by launch.spawn_ranks, gloo for
+the rendezvous and the frame's name): every step, each rank puts its
+interleaved band of the frame into the shared page-locked host frame
+(distributed.HostFrame) and raises its ready flag; rank 0 waits for all
+flags, keeps a copy of the frame and releases the slot.  Step s renders with
+seed + s, so a slot that rotated wrongly shows the wrong image.
+  mode cpu: the band comes from the CPU oracle and is written with numpy, the
+            flag by a host store (the shared-memory protocol without a GPU)
+  mode gpu: the band is rendered straight into the frame on cuda:0
+            (HostFrame.render: out_row_stride, pt_signal), lanes_per_pixel 4
+Rank 0 saves the frames, (steps, H, W, 3) float32, to argv[1]."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from pathtracerpython_amd import _native, scene_reader  # noqa: E402
+from pathtracerpython_amd.distributed import HostFrame  # noqa: E402
+from pathtracerpython_amd.launch import pg_timeout, rank_env  # noqa: E402
+
+
+def main():
+    out, W, H, spp, B, seed, steps = sys.argv[1], *map(int, sys.argv[2:8])
+    mode = sys.argv[8]
+    rank, local, world = rank_env()
+    dist.init_process_group("gloo", timeout=pg_timeout())
+    name = [HostFrame.new_name() if rank == 0 else None]
+    dist.broadcast_object_list(name, src=0)
+    if rank == 0:
+        hf = HostFrame(H, W, world, rank, name[0], create=True, map_device=(mode == "gpu"))
+    dist.barrier()
+    if rank != 0:
+        hf = HostFrame(H, W, world, rank, name[0], map_device=(mode == "gpu"))
+    scene_reader.VERBOSE = False
+    sc = scene_reader.Scene(os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl"))
+    frames = []
+    if mode == "gpu":
+        import torch
+        from pathtracerpython_amd.render import Renderer
+        torch.cuda.set_device(0)
+        r = Renderer(sc)
+        s = torch.cuda.current_stream().cuda_stream
+    else:
+        from oracle import oracle
+        from pathtracerpython_amd.pack import pack_scene
+        pk = pack_scene(sc)
+    lib = _native.lib()
+    for step in range(steps):
+        if mode == "gpu":
+            p = r.params(W, H, spp, B, seed + step, row_step=world, row_phase=rank, lanes_per_pixel=4)
+            hf.render(r, p, step, s, timeout_s=60)
+        else:
+            need = step - hf.slots + 1   # as HostFrame.render: the slot's last user released
+            if need > 0:
+                _native.check(lib.pt_wait_flags(C.c_void_p(hf.host + hf.RELEASED + 64 * (step % hf.slots)),
+                                                1, 8, need, 60.0), "pt_wait_flags")
+            pix = np.array([ix * H + iy for iy in hf.band_rows for ix in range(W)], dtype=np.int64)
+            cols, _ = oracle.render(pk, W, H, spp, B, seed + step, pixels=pix, threads=1)
+            f = hf.frame(step)
+            for j, iy in enumerate(hf.band_rows):
+                f[H - 1 - iy] = cols[j * W:(j + 1) * W]
+            del f
+            hf.u64[(hf.READY + 64 * rank) // 8] = step + 1
+        if rank == 0:
+            frames.append(hf.wait(step, timeout_s=60).copy())
+            hf.release(step)
+    if mode == "gpu":
+        torch.cuda.synchronize()
+        r.close()
+    dist.barrier()
+    hf.close()
+    if rank == 0:
+        np.save(out, np.stack(frames))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

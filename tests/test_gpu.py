@@ -628,3 +628,42 @@ def test_host_frame_bands_in_one_process(cornell, world):
         finally:
             for hf in frames[::-1]:
                 hf.close()
+
+
+def test_host_frame_two_rank_processes(cornell, tmp_path):
+    """Two rank processes on device 0 (gloo rendezvous) render their bands
+    straight into one shared page-locked frame, five steps with a new seed
+    each (slot rotation); rank 0's frames equal one render each, bit for bit
+    (lanes_per_pixel 4 everywhere)."""
+    from conftest import ROOT
+    from pathtracerpython_amd.launch import spawn_ranks
+    W, H, spp, B, seed, steps = 64, 37, 16, 4, 11, 5
+    out = str(tmp_path / "frames.npy")
+    rc = spawn_ranks(2, [os.path.join(ROOT, "tests", "rank_worker_hostframe.py"), out, str(W), str(H),
+                         str(spp), str(B), str(seed), str(steps), "gpu"])
+    assert rc == 0
+    got = np.load(out)
+    with Renderer(cornell) as r:
+        for s in range(steps):
+            ref = r.render_params(r.params(W, H, spp, B, seed + s, lanes_per_pixel=4))
+            assert np.array_equal(got[s], ref), s
+
+
+def test_bench_host_frame_path_two_ranks(tmp_path):
+    """bench.py's N > 1 host-frame path on one GPU (PT_BENCH_REHEARSE: two
+    self-spawned ranks on device 0 over gloo): the line is printed, and the
+    frame rank 0 read from host memory matches the oracle over every pixel."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, PT_BENCH_REHEARSE="1")
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6",
+                          "--warmup", "2", "--no-cpu-baseline"], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    line = json.loads([ln for ln in res.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["frame"] == "host"
+    assert line["linf_checked"] == "all 262144 pixels" and line["pixels_over"]["1e-6"] == 0
+    legs = line["frame_modes"]["host"]["legs_ms"]
+    assert legs["band_kernel_max"] >= legs["band_kernel_min"] > 0

@@ -149,7 +149,49 @@ def k5(tmp_path_factory):
     return scene_reader.Scene(write_k5_scene(str(d), n_tris=100_000, seed=0, size=1024))
 
 
-def test_k5_full(k5):
+@pytest.fixture(scope="module")
+def k5_frame(k5):
+    """The full K5 frame (1024x1024, 256 spp, 4 bounces, f64) and the scene."""
+    with Renderer(k5) as r:
+        fb = render_dev(r, r.params(1024, 1024, 256, 4, 9, out_f64=True))
+        return r.packed, fb
+
+
+def test_k5_full_row_vs_oracle(k5, k5_frame):
+    """A whole image row (1,024 pixels) of the full K5 frame against the
+    oracle.  The oracle brute-forces all 100k triangles per ray (~7 ms per
+    path sample on 16 threads: a row at 256 spp would take ~30 min), so the
+    row is checked through the keyed RNG's sample independence:
+      1. the frame's row equals the mean of its 128 two-sample slices
+         (spp 2, sample_begin 2c), each rendered as its own launch of that
+         row — to rounding (only the order of the sums differs);
+      2. the oracle renders three of those slices (c = 0, 64, 127) over the
+         whole row, <= 1e-12 each.
+    Every sample of the row is thus computed by the GPU in two different
+    launches, and 6 of its 256 by the oracle too."""
+    packed, fb = k5_frame
+    W = H = 1024
+    iy0 = 600
+    row = fb[H - 1 - iy0]
+    slices = {}
+    with Renderer(k5) as r:
+        acc = np.zeros((W, 3))
+        for c in range(128):
+            sl = render_dev(r, r.params(W, H, 2, 4, 9, out_f64=True, row_begin=iy0, row_end=iy0 + 1,
+                                        sample_begin=2 * c))[0]
+            acc += sl
+            if c in (0, 64, 127):
+                slices[c] = sl
+    mean = acc / 128
+    assert np.abs(mean - row).max() <= 1e-12 * max(1.0, np.abs(row).max())
+    pix = np.array([ix * H + iy0 for ix in range(W)], dtype=np.int64)
+    for c, sl in slices.items():
+        ref, _ = oracle.render(packed, W, H, 2, 4, 9, pixels=pix, sample_begin=2 * c)
+        err = float(np.abs(sl - ref).max())
+        assert err <= TOL, (c, err)
+
+
+def test_k5_full(k5, k5_frame):
     """K5: 100k-triangle synthetic mesh, 1024x1024, 256 spp, 4 bounces (the
     wavefront path, ~2 s).  Oracle (brute force over all triangles) on 16
     pixels over bottom, middle and top rows; finite everywhere; the whole
@@ -158,10 +200,9 @@ def test_k5_full(k5):
     bitwise equal between the wavefront, the single kernel and the forced-f64
     kernel."""
     W = H = 1024
+    packed, fb = k5_frame
     with Renderer(k5) as r:
-        packed = r.packed
         assert r.packed.n_tri == 100_012
-        fb = render_dev(r, r.params(W, H, 256, 4, 9, out_f64=True))
         assert np.isfinite(fb).all()
         mk = render_dev(r, r.params(W, H, 256, 4, 9, out_f64=True, megakernel=True))
         assert np.array_equal(fb, mk), np.abs(fb - mk).max()

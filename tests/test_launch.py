@@ -76,3 +76,43 @@ def test_cli_devices_flag_parses():
     from pathtracerpython_amd.main import setup
     a = setup(["scene.sdl", "--devices", "4", "-r", "8"])
     assert a.devices == 4 and a.n_rays == 8
+
+
+@pytest.mark.parametrize("world,H", [(2, 12), (8, 13)])
+def test_host_frame_protocol_gloo(tmp_path, packed, world, H):
+    """distributed.HostFrame across rank processes without a GPU: the shared
+    /dev/shm frame, the ready flags, pt_wait_flags and the two-slot rotation
+    (each step a different seed) — rank 0's frames equal the oracle's."""
+    from oracle import oracle
+    from pathtracerpython_amd.launch import spawn_ranks
+    from pathtracerpython_amd.render import from_list_order
+    W, spp, B, seed, steps = 10, 2, 3, 9, 5
+    out = str(tmp_path / "frames.npy")
+    rc = spawn_ranks(world, [os.path.join(ROOT, "tests", "rank_worker_hostframe.py"), out,
+                             str(W), str(H), str(spp), str(B), str(seed), str(steps), "cpu"])
+    assert rc == 0
+    got = np.load(out)
+    assert got.shape == (steps, H, W, 3)
+    for s in range(steps):
+        full, _ = oracle.render(packed, W, H, spp, B, seed + s)
+        assert np.array_equal(got[s], from_list_order(full, W, H).astype(np.float32)), s
+
+
+def test_host_frame_file_lifecycle():
+    """Rank 0 creates the shared file exclusively and removes it on close;
+    the slots and the rows of each band are where render() puts them."""
+    from pathtracerpython_amd.distributed import HostFrame
+    name = HostFrame.new_name()
+    a = HostFrame(13, 10, 4, 0, name, create=True, map_device=False)
+    with pytest.raises(FileExistsError):
+        HostFrame(13, 10, 4, 0, name, create=True, map_device=False)
+    b = HostFrame(13, 10, 4, 3, name, map_device=False)
+    assert b.band_rows == [11, 7, 3] and a.band_rows == [12, 8, 4, 0]
+    b.frame(1)[0, 0, 0] = 7.0
+    assert a.frame(3)[0, 0, 0] == 7.0 and a.frame(0)[0, 0, 0] == 0.0   # 2 slots
+    assert a.band_target(0) == (None, 0)   # no device mapping
+    with pytest.raises(ValueError):
+        a.render(None, None, 0, None)
+    b.close()
+    a.close()
+    assert not os.path.exists(os.path.join("/dev/shm", name))
