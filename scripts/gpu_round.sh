@@ -10,7 +10,7 @@
 # Each GPU step has its own time limit; a failed test run stops before the
 # measurements, a fault or timeout stops everything.
 set -o pipefail
-TAG=${1:-r03}
+TAG=${1:-r04}
 OUT=gpurun_out/round_$TAG
 mkdir -p "$OUT"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \

@@ -12,13 +12,14 @@
 #   2. k_render SQ counters (busy, stalls, instruction mix) -> TAG_pmc_k2_sq.json
 #   3. kernel trace + stats of the K2 bench command -> TAG_k2_kernel_stats.csv
 #   4. the K2 bench line -> TAG_bench_k2.json
-#   5. K5: kernel stats of the bench render, HBM traffic of the shadow walks
+#   5. K5: kernel stats of the bench render and of a serialised-walks render
+#      (each walk's own time), HBM traffic of the shadow walks
 #      (traffic_k5.json, stamped) and of the closest walks, the K5 bench line
 # Usage (from the repo root): gpurun -- bash scripts/refresh_profiles.sh TAG
 # Every GPU step runs under its own time limit; the script stops at the first
 # failure.
 set -euo pipefail
-TAG=${1:-r03}
+TAG=${1:-r04}
 R=$PWD
 OUT=$R/gpurun_out/refresh_$TAG
 P=$OUT/profiles
@@ -56,6 +57,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     > "$OUT/trace_k5.log" 2>&1
 cp "$OUT/trace_k5/k5_kernel_stats.csv" "$P/${TAG}_k5_kernel_stats.csv"
 cd /tmp
+# the walks' own times (bench.py's k5 roofline: a PT_FLAG_KERNEL_TIMES render,
+# the two walks of a step one after the other)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_k5s" -o k5 \
+    -- python3 "$R/scripts/prof_k5_serial.py" 1 > "$OUT/trace_k5s.log" 2>&1
+cp "$OUT/trace_k5s/k5_kernel_stats.csv" "$P/${TAG}_k5_kernel_stats_serial.csv"
 pmc k5_fetch FETCH_SIZE "$R/scripts/prof_k5.py" 1 1024 256
 pmc k5_write WRITE_SIZE "$R/scripts/prof_k5.py" 1 1024 256
 PMC_KERNEL=k_wf_shadow python3 "$R/scripts/summarize_pmc.py" "$P/${TAG}_pmc_k5_traffic.json" \
