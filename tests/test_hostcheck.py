@@ -166,6 +166,23 @@ def test_bvh_structure_and_conservative_pruning(hostcheck, tmp_path, n_tris, see
     assert checked > 100 and missed == 0
 
 
+def test_qbvh_clustered_tiny_triangles(hostcheck, tmp_path):
+    """clusters of tiny and sliver triangles make BVH nodes far
+    smaller than their distance from the origin.  The 4-wide nodes still
+    quantise (the builder's empty-box check, pt_prepare.h QBuilder: an absent
+    child's box must stay empty after rounding), no line meets an absent
+    child, and pruning never drops a triangle the f64 line meets; the
+    host wavefront render equals the single kernel's."""
+    from conftest import clustered_scene
+    pk = pack_scene(clustered_scene(tmp_path, 600, 4))
+    out = (C.c_int64 * 5)()
+    assert hostcheck.hc_qbvh_check(C.byref(pk.desc), C.c_int64(150), C.c_uint64(4), out) == 0
+    missed, checked, nq, slab_diff, slab_n = list(out)
+    assert nq > 1 and checked > 50 and missed == 0
+    assert slab_n > 1000 and slab_diff == 0
+    _wavefront_case(hostcheck, pk, 14, 14, 2, 4, 5)
+
+
 @pytest.mark.parametrize("n_tris,seed", [(300, 1), (2000, 2)])
 def test_qbvh_walk_conservative(hostcheck, tmp_path, n_tris, seed):
     """The wavefront walks' 4-wide child test (q_child_dist: one fma per slab
