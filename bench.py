@@ -314,13 +314,34 @@ def main():
     assert rows == len(band_rows_of(H, rank, world))
     stream = torch.cuda.current_stream()
     name = bcast(HostFrame.new_name() if rank == 0 else None)
-    if world > 1:
-        dist.barrier()   # rank 0 creates the file first
-    hf = HostFrame(H, W, world, rank, name, create=(rank == 0)) if rank == 0 else None
+    # the shared host frame (rank 0 creates the file first); if any rank
+    # cannot map it (no /dev/shm, page-locking refused), every rank falls back
+    # to the device-frame transport and the line says why
+    hf, hf_err = None, None
+
+    def open_frame(create):
+        try:
+            return HostFrame(H, W, world, rank, name, create=create), None
+        except Exception as e:   # noqa: BLE001 (reported in the line)
+            return None, f"rank {rank}: {type(e).__name__}: {e}"
+    if rank == 0:
+        hf, hf_err = open_frame(True)
     if world > 1:
         dist.barrier()
         if rank != 0:
-            hf = HostFrame(H, W, world, rank, name)
+            hf, hf_err = open_frame(False)
+        errs = [None] * world
+        dist.all_gather_object(errs, hf_err)
+        hf_err = next((e for e in errs if e), None)
+    if hf_err:
+        if hf is not None:
+            hf.close()
+            hf = None
+        if args.frame == "host":
+            args.frame = "device"
+            if rank == 0:
+                print(f"bench: host frame unavailable ({hf_err}); timing the device frame",
+                      file=sys.stderr, flush=True)
     ctx = dict(r=r, p=p, hf=hf, stream=stream.cuda_stream, rank=rank, world=world, dist=dist,
                H=H, W=W, max_rows=(H + world - 1) // world)
     paths = W * H * SPP
@@ -356,7 +377,8 @@ def main():
             if rehearse else device_mode()
     else:
         head = device_mode()
-        other = host_mode(0)
+        other = host_mode(0) if hf is not None else {"skipped": f"host frame unavailable: {hf_err}",
+                                                     "_fb": None}
     modes = {args.frame: head, ("device" if args.frame == "host" else "host"): other}
     k_ms = head["_k_ms"]
     fb = head["_fb"]
@@ -435,6 +457,7 @@ def main():
                                       if args.frame == "host" else
                                       "RCCL gather + device assembly (N > 1) + D2H copy")},
             "frame_modes": modes,
+            "host_frame_error": hf_err,
             "linf_vs_cpu_ref": linf, "linf_checked": checked, "pixels_over": over,
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -442,7 +465,8 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
-    hf.close()
+    if hf is not None:
+        hf.close()
     r.close()
     if world > 1:
         dist.barrier()
