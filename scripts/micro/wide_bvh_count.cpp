@@ -55,6 +55,117 @@ struct WTree {
         return me;
     }
 };
+// SAH-optimal collapse of the two-child tree into N-wide nodes (dynamic
+// programme after Ylitie, Karras & Laine 2017, section 3.1): cost of a node
+// visit 1 per unit of box area, of a leaf-unit test cl; D(x, j) = the least
+// cost of subtree x spread over j child slots of its parent.
+struct DpCollapse {
+    const HostScene& H;
+    int N;
+    double cl;
+    struct Box { float lo[3], hi[3]; };
+    std::vector<std::vector<double>> D;     // [cnode][j], j = 1..N
+    std::vector<std::vector<int>> how;      // [cnode][j]: 0 = one slot, -1 = as j-1, k > 0 = split (k, j-k)
+    std::vector<double> A;                  // box area of each cnode
+    static double area(const float* lo, const float* hi) {
+        const double e0 = (double)hi[0] - lo[0], e1 = (double)hi[1] - lo[1], e2 = (double)hi[2] - lo[2];
+        return e0 * e1 + e1 * e2 + e2 * e0;
+    }
+    DpCollapse(const HostScene& h, int n, double c) : H(h), N(n), cl(c) {
+        const size_t m = H.cnode.size();
+        D.assign(m, std::vector<double>(N + 1, 0.0));
+        how.assign(m, std::vector<int>(N + 1, 0));
+        A.assign(m, 0.0);
+        std::vector<char> done(m, 0);
+        // post-order over the internal nodes
+        std::vector<std::pair<int, int>> st;
+        if (H.k.bvh_root >= 0) st.push_back({H.k.bvh_root, 0});
+        while (!st.empty()) {
+            auto [r, phase] = st.back();
+            st.pop_back();
+            const CNode& C = H.cnode[r];
+            if (phase == 0) {
+                st.push_back({r, 1});
+                if (C.c0 >= 0) st.push_back({C.c0, 0});
+                if (C.c1 >= 0) st.push_back({C.c1, 0});
+                continue;
+            }
+            float lo[3], hi[3];
+            for (int a = 0; a < 3; ++a) { lo[a] = std::min(C.lo0[a], C.lo1[a]); hi[a] = std::max(C.hi0[a], C.hi1[a]); }
+            A[r] = area(lo, hi);
+            const double a0 = area(C.lo0, C.hi0), a1 = area(C.lo1, C.hi1);
+            auto Dc = [&](int x, double ax, int j) { return x < 0 ? ax * cl : D[x][j]; };
+            // as one wide node: its visit + the best spread of the N slots
+            double node = INFINITY;
+            for (int j = 1; j < N; ++j) node = std::min(node, Dc(C.c0, a0, j) + Dc(C.c1, a1, N - j));
+            node += A[r];
+            D[r][1] = node;
+            how[r][1] = 0;
+            for (int j = 2; j <= N; ++j) {
+                D[r][j] = D[r][j - 1];
+                how[r][j] = -1;
+                for (int k = 1; k < j; ++k) {
+                    const double c = Dc(C.c0, a0, k) + Dc(C.c1, a1, j - k);
+                    if (c < D[r][j]) { D[r][j] = c; how[r][j] = k; }
+                }
+            }
+        }
+    }
+    // the slots of subtree x spread over j slots: (ref, box) pairs
+    void expand(int x, const float* lo, const float* hi, int j, std::vector<std::pair<int32_t, Box>>* out) const {
+        Box b;
+        for (int a = 0; a < 3; ++a) { b.lo[a] = lo[a]; b.hi[a] = hi[a]; }
+        if (x < 0) { out->push_back({x, b}); return; }
+        while (j > 1 && how[x][j] == -1) --j;
+        if (j == 1 || how[x][j] == 0) { out->push_back({x, b}); return; }
+        const int k = how[x][j];
+        const CNode& C = H.cnode[x];
+        expand(C.c0, C.lo0, C.hi0, k, out);
+        expand(C.c1, C.lo1, C.hi1, j - k, out);
+    }
+    // children of the wide node made from cnode r
+    void children(int r, std::vector<std::pair<int32_t, Box>>* out) const {
+        const CNode& C = H.cnode[r];
+        const double a0 = area(C.lo0, C.hi0), a1 = area(C.lo1, C.hi1);
+        auto Dc = [&](int x, double ax, int j) { return x < 0 ? ax * cl : D[x][j]; };
+        int best = 1;
+        double bc = INFINITY;
+        for (int j = 1; j < N; ++j) {
+            const double c = Dc(C.c0, a0, j) + Dc(C.c1, a1, N - j);
+            if (c < bc) { bc = c; best = j; }
+        }
+        expand(C.c0, C.lo0, C.hi0, best, out);
+        expand(C.c1, C.lo1, C.hi1, N - best, out);
+    }
+};
+
+struct WTreeDp {
+    // builds WNodes with DpCollapse's child choice
+    static int32_t build(WTree& T, const DpCollapse& P, int32_t ref) {
+        if (ref < 0) return ref;
+        std::vector<std::pair<int32_t, DpCollapse::Box>> ch;
+        P.children(ref, &ch);
+        const int32_t me = (int32_t)T.node.size();
+        T.node.push_back(WNode{});
+        WNode W{};
+        W.n = (int)ch.size();
+        for (int c = 0; c < W.n; ++c)
+            for (int a = 0; a < 3; ++a) { W.lo[c][a] = ch[c].second.lo[a]; W.hi[c][a] = ch[c].second.hi[a]; }
+        for (int c = 0; c < W.n; ++c) W.ref[c] = build(T, P, ch[c].first);
+        T.node[me] = W;
+        return me;
+    }
+};
+int g_build = 0;      // 0: open the largest-area child (QBuilder's rule); 1: SAH dynamic programme
+// bounce-0 occluder hint experiment: [0] bounce-0 shadow rays walked, [1] with a hint,
+// [2] closed by the walk, [3] closed by the hint alone, [4] node visits of those,
+// [5] node visits of all bounce-0 walks
+int64_t g_hint[6];
+std::vector<int> g_hint_unit;
+bool g_hint_hit_pending = false;
+ShadowTrav1 tv_dummy;
+double g_cleaf = 0.33;
+
 struct Count { int64_t queries = 0, visits = 0, boxes = 0, leaves = 0, units = 0, mismatches = 0, maxstack = 0; };
 
 int g_order = 0;   // 0: all children nearest-first; 1: the nearest first, the rest in node order
@@ -150,13 +261,21 @@ extern "C" {
 // (14 per N), then the shipped walks' stats (8: hc_render_wavefront's walk_stats)
 int wx_count(const pt_scene_desc* d, const pt_render_params* p, int64_t* out, int order) {
     g_order = order;
+    if (const char* b = getenv("WX_BUILD")) g_build = atoi(b);
+    if (const char* c = getenv("WX_CLEAF")) g_cleaf = atof(c);
     HostScene H;
     if (!prepare_scene(d, &H).empty()) return -1;
     bind_host(&H);
     if (H.k.n_bnode == 0 || H.k.n_qnode == 0 || H.k.qstack > kBvhStack) return -3;
     WTree T4, T8;
-    T4.root = T4.build(H, H.k.bvh_root, 4);
-    T8.root = T8.build(H, H.k.bvh_root, 8);
+    if (g_build == 1) {
+        const DpCollapse P4(H, 4, g_cleaf), P8(H, 8, g_cleaf);
+        T4.root = WTreeDp::build(T4, P4, H.k.bvh_root);
+        T8.root = WTreeDp::build(T8, P8, H.k.bvh_root);
+    } else {
+        T4.root = T4.build(H, H.k.bvh_root, 4);
+        T8.root = T8.build(H, H.k.bvh_root, 8);
+    }
     Count cs[2], cc[2];
     int64_t ws[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int32_t first, rows;
@@ -185,6 +304,8 @@ int wx_count(const pt_scene_desc* d, const pt_render_params* p, int64_t* out, in
         }
     }
     std::vector<uint32_t> want(n);
+    g_hint_unit.assign(n * 3, -1);
+    memset(g_hint, 0, sizeof g_hint);
     for (int step = 0;; ++step) {
         bool any = false;
         for (size_t i = 0; i < n; ++i) {
@@ -210,16 +331,42 @@ int wx_count(const pt_scene_desc* d, const pt_render_params* p, int64_t* out, in
                 const ShadowStack K{buf, 1};
                 s1_init(T, H.k, o32, ogrp, r, H.k.qroot);
                 ++ws[0];
+                // hint experiment: the unit that closed this slot's previous
+                // bounce-0 ray k, tested alone first
+                const bool b0 = W[i].b() == 0;
+                if (b0) {
+                    ++g_hint[0];
+                    const int hu = g_hint_unit[i * 3 + k];
+                    if (hu >= 0) {
+                        ++g_hint[1];
+                        Shadow1 rh = r0;
+                        tv_dummy.o32 = o32; tv_dummy.ogrp = ogrp;
+                        if (H.k.bunitc) shadow1_unit(H.k, bvh_unit<true>(H.k, hu), o32, ogrp, &rh, sp);
+                        else shadow1_unit(H.k, bvh_unit<false>(H.k, hu), o32, ogrp, &rh, sp);
+                        if (!shadow1_open(H.k, rh)) g_hint_hit_pending = true;
+                    }
+                }
+                int64_t v0 = ws[1];
+                int closer = -1;
                 while (T.ref != kNoRef) {
                     while (T.ref >= 0) { s1_qnode(T, K, H.k, r); ++ws[1]; }
                     if (T.ref != kNoRef) {
                         ++ws[2];
                         ws[3] += (~T.ref) & 7;
+                        const bool was_open = shadow1_open(H.k, r);
                         if (H.k.bunitc) s1_units<true>(T, H.k, &r, sp, T.ref);
                         else s1_units<false>(T, H.k, &r, sp, T.ref);
+                        if (was_open && !shadow1_open(H.k, r)) closer = ~T.ref >> 3;
                         T.ref = s1_pop(T, K, H.k, r);
                     }
                 }
+                if (b0) {
+                    if (!shadow1_open(H.k, r)) ++g_hint[2];          // bounce-0 rays closed by the BVH
+                    if (g_hint_hit_pending) { ++g_hint[3]; g_hint[4] += ws[1] - v0; }   // visits a hint saves
+                    g_hint[5] += ws[1] - v0;
+                    g_hint_unit[i * 3 + k] = closer;   // (-1: open: no hint next time)
+                }
+                g_hint_hit_pending = false;
                 shadow_wide(T4, H.k, o32, ogrp, r0, sp, &cs[0], r);
                 shadow_wide(T8, H.k, o32, ogrp, r0, sp, &cs[1], r);
                 wf_put_shadow1(&SQ[i], r);
@@ -258,6 +405,9 @@ int wx_count(const pt_scene_desc* d, const pt_render_params* p, int64_t* out, in
         }
     }
     memcpy(out + 28, ws, sizeof ws);
+    fprintf(stderr, "hint: bounce0_rays %lld with_hint %lld closed %lld hint_closes %lld visits_saved %lld bounce0_visits %lld all_shadow_visits %lld\n",
+            (long long)g_hint[0], (long long)g_hint[1], (long long)g_hint[2], (long long)g_hint[3],
+            (long long)g_hint[4], (long long)g_hint[5], (long long)ws[1]);
     return 0;
 }
 }
