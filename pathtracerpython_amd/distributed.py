@@ -115,10 +115,13 @@ def assemble_bands_device(gathered, out, stream=None):
 
 
 def render_distributed(renderer, width, height, spp=1, bounces=1, seed=None, rr=False,
-                       rr_depth=3, group=None, return_tiles=False):
+                       rr_depth=3, group=None, return_tiles=False, transport="device"):
     """Render `height` rows interleaved over the ranks of `group` on each
     rank's current CUDA/HIP device; returns the framebuffer (float32 numpy) on
-    rank 0 and None on the other ranks."""
+    rank 0 and None on the other ranks.
+    transport "device": each band into a device tile, one gather to rank 0
+    (RCCL with the nccl backend); "host": every band straight into one shared
+    page-locked host frame (HostFrame; the ranks of one node)."""
     import torch
     import torch.distributed as dist
     rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -126,6 +129,28 @@ def render_distributed(renderer, width, height, spp=1, bounces=1, seed=None, rr=
     rb, re, step, phase = rank_band(height, rank, world)
     p = renderer.params(width, height, spp, bounces, seed, rr, rr_depth, row_begin=rb,
                         row_end=re, row_step=step, row_phase=phase)
+    if transport == "host":
+        if return_tiles:
+            raise ValueError("return_tiles needs the device transport")
+        name = [HostFrame.new_name() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(name, src=0, group=group)
+        hf = HostFrame(height, width, world, rank, name[0], create=True) if rank == 0 else None
+        if world > 1:
+            dist.barrier(group=group)
+            if rank != 0:
+                hf = HostFrame(height, width, world, rank, name[0])
+        try:
+            hf.render(renderer, p, 0, torch.cuda.current_stream().cuda_stream)
+            fb = hf.wait(0).copy() if rank == 0 else None
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier(group=group)
+        finally:
+            hf.close()
+        return fb
+    if transport != "device":
+        raise ValueError(f"transport must be 'device' or 'host', not {transport!r}")
     rows = max_band_rows(height, world)
     tile = torch.zeros((rows, width, 3), dtype=torch.float32, device="cuda")
     renderer.render_device(p, tile.data_ptr(), torch.cuda.current_stream().cuda_stream)

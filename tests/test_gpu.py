@@ -469,6 +469,7 @@ def test_kernel_timing_and_distributed_world1(R):
     fb = render_distributed(R, 64, 48, spp=2, bounces=3, seed=1)
     assert R.last_kernel_ms() > 0
     assert np.array_equal(fb, R.render(64, 48, 2, 3, 1))
+    assert np.array_equal(render_distributed(R, 64, 48, spp=2, bounces=3, seed=1, transport="host"), fb)
     assert torch.cuda.is_available()
 
 
