@@ -50,25 +50,35 @@ def main():
         from pathtracerpython_amd.pack import pack_scene
         pk = pack_scene(sc)
     lib = _native.lib()
-    for step in range(steps):
+
+    def publish(step):   # this rank's band of `step` into the frame, then its flag
         if mode == "gpu":
             p = r.params(W, H, spp, B, seed + step, row_step=world, row_phase=rank, lanes_per_pixel=4)
             hf.render(r, p, step, s, timeout_s=60)
-        else:
-            need = step - hf.slots + 1   # as HostFrame.render: the slot's last user released
-            if need > 0:
-                _native.check(lib.pt_wait_flags(C.c_void_p(hf.host + hf.RELEASED + 64 * (step % hf.slots)),
-                                                1, 8, need, 60.0), "pt_wait_flags")
-            pix = np.array([ix * H + iy for iy in hf.band_rows for ix in range(W)], dtype=np.int64)
-            cols, _ = oracle.render(pk, W, H, spp, B, seed + step, pixels=pix, threads=1)
-            f = hf.frame(step)
-            for j, iy in enumerate(hf.band_rows):
-                f[H - 1 - iy] = cols[j * W:(j + 1) * W]
-            del f
-            hf.u64[(hf.READY + 64 * rank) // 8] = step + 1
-        if rank == 0:
+            return
+        need = step - hf.slots + 1   # as HostFrame.render: the slot's last user released
+        if need > 0:
+            _native.check(lib.pt_wait_flags(C.c_void_p(hf.host + hf.RELEASED + 64 * (step % hf.slots)),
+                                            1, 8, need, 60.0), "pt_wait_flags")
+        pix = np.array([ix * H + iy for iy in hf.band_rows for ix in range(W)], dtype=np.int64)
+        cols, _ = oracle.render(pk, W, H, spp, B, seed + step, pixels=pix, threads=1)
+        f = hf.frame(step)
+        for j, iy in enumerate(hf.band_rows):
+            f[H - 1 - iy] = cols[j * W:(j + 1) * W]
+        del f
+        hf.u64[(hf.READY + 64 * rank) // 8] = step + 1
+
+    # bench.py's order: rank 0 queues step s + 1 before it waits for step s
+    if rank == 0:
+        publish(0)
+        for step in range(steps):
+            if step + 1 < steps:
+                publish(step + 1)
             frames.append(hf.wait(step, timeout_s=60).copy())
             hf.release(step)
+    else:
+        for step in range(steps):
+            publish(step)
     if mode == "gpu":
         torch.cuda.synchronize()
         r.close()
