@@ -566,9 +566,9 @@ PT_HD D3 shadow_color(const SceneK& S, int obj, const ShadowSet& sh, Counters* c
     const Mat& m = S.mat[obj];
     const Mat& lm = S.mat[sh.leak];   // main.py:70
     bump<COUNT>(cnt, &Counters::shading_points, 1);
-    return d3(m.rgb[0] * m.ka * S.ambient + S.light_rgb[0] * lm.rgb[0] * dsum,
-              m.rgb[1] * m.ka * S.ambient + S.light_rgb[1] * lm.rgb[1] * dsum,
-              m.rgb[2] * m.ka * S.ambient + S.light_rgb[2] * lm.rgb[2] * dsum);
+    // m.rgb * m.ka * S.ambient + S.light_rgb * lm.rgb * dsum, the two
+    // products precomputed per object (Mat::amb, Mat::lrgb)
+    return d3(m.amb[0] + lm.lrgb[0] * dsum, m.amb[1] + lm.lrgb[1] * dsum, m.amb[2] + lm.lrgb[2] * dsum);
 }
 
 // ------------------------------------------------------------------ BVH --

@@ -744,6 +744,10 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
         M.ka = m[3]; M.kd = m[4]; M.ks = m[5];
         M.kdks = m[4] + m[5];
         M.nexp = m[7];
+        for (int c = 0; c < 3; ++c) {
+            M.amb[c] = m[c] * m[3] * d->ambient;
+            M.lrgb[c] = d->light_rgb[c] * m[c];
+        }
         M.nint = (m[7] >= 0 && m[7] <= 16 && m[7] == floor(m[7])) ? (int32_t)m[7] : -1;
     }
     // light CDF: running sums from 0, utils.py:30-35

@@ -3,7 +3,7 @@
 # --pmc pass (TCC_HIT_sum TCC_MISS_sum: the walks' L2 hit rate), summarised
 # per walk kernel (dev tool).  Usage: bash scripts/exp_k5_working_set.sh OUTDIR
 set -uo pipefail
-R=$PWD; OUT=${1:-$R/gpurun_out/k5ws}; mkdir -p "$OUT"
+R=$PWD; OUT=$(readlink -f "${1:-$R/gpurun_out/k5ws}"); mkdir -p "$OUT"
 timeout -k 10 400 python3 "$R/scripts/exp_k5_working_set.py" > "$OUT/times.jsonl" 2> "$OUT/times.err" || exit 1
 grep -v amdgpu "$OUT/times.jsonl"
 cd /tmp && export TMPDIR=/tmp
