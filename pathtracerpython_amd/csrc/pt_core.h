@@ -210,7 +210,16 @@ struct SceneK {
                                  // coplanar pair or degenerate: the walks read bunit)
     float bvh_eh, bvh_eq, bvh_qhi;   // maxima over bunit
     int32_t bvh_obj1;            // the BVH's one object, or -1 (several: from tri_obj)
+    // The f64 constants the bounce loop reads (eye, the frame centres,
+    // light_sum, light_rgb),
+    // also in device memory, where the loop reads them: as kernel-argument
+    // fields they sit next to `ortho` and came in one 16-dword scalar load
+    // whose register tuple was spilled to VGPR lanes and restored whole at
+    // each use (336 v_readlane in k_render; 99 -> 73 SGPR spills, 499 -> 109
+    // readlanes with this table)
+    const double* kd;            // [kKd*] below
 };
+enum : int { kKdEye = 0, kKdCenterS = 3, kKdLightSum = 6, kKdCenter = 7, kKdLightRgb = 10, kKdCount = 13 };
 
 // ------------------------------------------------------------------ RNG --
 // Philox4x32-10 (Salmon et al., SC'11), key = seed, counter =
@@ -386,7 +395,7 @@ PT_HD int verdict_code(Verdict v) { return v.cand ? kCand : (v.amb ? kAmb : kMis
 // ------------------------------------------------------ light sampling --
 // pick_random_triangle, utils.py:28-39: first i with cum[i] <= n < cum[i+1]
 PT_HD int pick_light(const SceneK& S, double u) {
-    const double n = 0.0 + (S.light_sum - 0.0) * u;
+    const double n = 0.0 + (S.kd[kKdLightSum] - 0.0) * u;
     for (int i = 0; i < S.n_light; ++i)
         if (S.light_cum[i] <= n && n < S.light_cum[i + 1]) return i;
     return 0;   // unreachable for u < 1 (the reference would fail here)

@@ -859,7 +859,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
         if (prop.multiProcessorCount > 0) s->n_cu = prop.multiProcessorCount;
     }
     HostScene& H = s->host;
-    constexpr int kArrays = 14;
+    constexpr int kArrays = 15;
     const size_t sz[kArrays] = {H.unit.size() * sizeof(UnitF), H.trid.size() * sizeof(TriD),
                                 H.tris.size() * sizeof(TriS), H.tri_obj.size() * sizeof(int32_t),
                                 H.mat.size() * sizeof(Mat), H.light_tri.size() * sizeof(int32_t),
@@ -867,11 +867,12 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
                                 H.tri_grp.size() * sizeof(int32_t),
                                 H.bnode.size() * sizeof(BNode), H.bunit.size() * sizeof(UnitF),
                                 H.cnode.size() * sizeof(CNode), H.qnode.size() * sizeof(QNode),
-                                H.bunitc.size() * sizeof(UnitC), H.unit_eye.size() * sizeof(UnitF)};
+                                H.bunitc.size() * sizeof(UnitC), H.unit_eye.size() * sizeof(UnitF),
+                                H.kd.size() * sizeof(double)};
     const void* src[kArrays] = {H.unit.data(), H.trid.data(), H.tris.data(), H.tri_obj.data(),
                                 H.mat.data(), H.light_tri.data(), H.light_cum.data(),
                                 H.tri_grp.data(), H.bnode.data(), H.bunit.data(), H.cnode.data(),
-                                H.qnode.data(), H.bunitc.data(), H.unit_eye.data()};
+                                H.qnode.data(), H.bunitc.data(), H.unit_eye.data(), H.kd.data()};
     size_t off[kArrays], total = 0;
     for (int i = 0; i < kArrays; ++i) { off[i] = total; total += align_up(sz[i]); }
     int rc = PT_OK;
@@ -900,6 +901,7 @@ int pt_scene_create(const pt_scene_desc* desc, pt_scene** out) {
     s->dev.qnode = (const QNode*)(b + off[11]);
     s->dev.bunitc = H.bunitc.empty() ? nullptr : (const UnitC*)(b + off[12]);
     s->dev.unit_eye = (const UnitF*)(b + off[13]);
+    s->dev.kd = (const double*)(b + off[14]);
     s->xb_surf = box_bound(H, false);
     s->xb_all = box_bound(H, true);
     *out = s;

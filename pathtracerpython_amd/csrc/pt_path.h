@@ -1492,7 +1492,7 @@ PT_HD D3 bounce(const SceneK& S, const TriS& R, const Mat& m, D3 P, D3 d_old,
     // "specular": r = 2 (n.d) n - d, normalised, rotated; k *= ks (e.r)^n
     const double nd2 = dot(n, d_old) * 2;
     const D3 r = unit(d3(nd2 * n.x - d_old.x, nd2 * n.y - d_old.y, nd2 * n.z - d_old.z));
-    const D3 e = unit(ld3(S.eye) - P);
+    const D3 e = unit(ld3(S.kd + kKdEye) - P);
     const D3 nd = rotate_y(R, r);
     *kf = m.ks * pow_ref(dot(e, nd), m);
     return nd;
@@ -1588,7 +1588,7 @@ struct LaneSched {
         if (++si >= J.n_samples) return false;
         *tri = tri0;
         sp.put3(kSpP, sp.get3(kSpP0));
-        sp.put3(kSpNd, d3(sp.get(kSpD0), sp.get(kSpD0 + 1), 0.0 - S.eye[2]));
+        sp.put3(kSpNd, d3(sp.get(kSpD0), sp.get(kSpD0 + 1), 0.0 - S.kd[kKdEye + 2]));
         if (COUNT) {
             bump<COUNT>(cnt, &Counters::closest_tests, (uint32_t)S.n_tri);
             bump<COUNT>(cnt, &Counters::ray_bounces, 1);
@@ -1662,7 +1662,7 @@ PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& 
         }
         // one pass: 3 shadow rays + the next ray's closest hit, same origin
         sp.put3(kSpNd, nd);
-        const F3 o32u = to_f3(P - ld3(S.center_s));   // the uniform units' frame
+        const F3 o32u = to_f3(P - ld3(S.kd + kKdCenterS));   // the uniform units' frame
         const F3 n32 = to_f3(unit(nd));
         ClosestAcc ca = closest_init();
         const bool any_trace = PT_WAVE_ANY(trace);
@@ -1692,7 +1692,7 @@ PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& 
         PT_STAMP(c2);
         PT_PHASE(1, c2 - c1);
         if (BVH && S.n_bnode) {   // the meshes: shadows as a packet, the closest ray ordered
-            const F3 o32 = to_f3(P - ld3(S.center));   // the BVH's frame
+            const F3 o32 = to_f3(P - ld3(S.kd + kKdCenter));   // the BVH's frame
             const bool ordered = !FORCE64 && S.bvh_depth < kBvhStack;
             if (ordered) {
                 bvh_shadow<COUNT>(S, o32, ogrp, &sh, sp, cnt);
@@ -1732,7 +1732,7 @@ PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& 
                 bump<COUNT>(cnt, &Counters::escapes, 1);
                 done = true;
             } else if (tn >= S.n_obj_tri) {   // light: main.py:214-215
-                acc = acc + ld3(S.light_rgb) * k;
+                acc = acc + ld3(S.kd + kKdLightRgb) * k;
                 bump<COUNT>(cnt, &Counters::light_hits, 1);
                 done = true;
             } else {
@@ -1761,7 +1761,7 @@ PT_HD D3 render_lane(const SceneK& S, const LaneJob& J, D3 d0, int tri0, D3 P0,
     D3 acc = d3(0, 0, 0);
     if (J.n_samples <= 0 || J.bounces <= 0) return acc;   // main.py:192 never runs
     if (tri0 < 0 || tri0 >= S.n_obj_tri) {   // primary ray escapes or hits the light
-        const D3 v = tri0 < 0 ? d3(0, 0, 0) : ld3(S.light_rgb);
+        const D3 v = tri0 < 0 ? d3(0, 0, 0) : ld3(S.kd + kKdLightRgb);
         for (int i = 0; i < J.n_samples; ++i) {
             acc = acc + v;
             if (COUNT) {

@@ -18,6 +18,7 @@
 namespace pt {
 
 struct HostScene {
+    std::vector<double> kd;       // SceneK::kd
     std::vector<UnitF> unit;
     std::vector<UnitF> unit_eye;
     std::vector<UnitF> bunit;
@@ -773,6 +774,14 @@ inline std::string prepare_scene(const pt_scene_desc* d, HostScene* H) {
     }
     for (int i = 0; i < 4; ++i) K.ortho[i] = d->ortho[i];
     K.ambient = d->ambient;
+    H->kd.assign(kKdCount, 0.0);
+    for (int i = 0; i < 3; ++i) {
+        H->kd[kKdEye + i] = K.eye[i];
+        H->kd[kKdCenterS + i] = K.center_s[i];
+        H->kd[kKdCenter + i] = K.center[i];
+        H->kd[kKdLightRgb + i] = K.light_rgb[i];
+    }
+    H->kd[kKdLightSum] = K.light_sum;
     // leaf codes (unit offset << 3 | count) travel in stack entries as
     // (~code << 3 | ray mask) in 32 bits
     if (H->bunit.size() >= (size_t(1) << 24)) return "mesh too large: at most 2^24 BVH units";
@@ -797,6 +806,7 @@ inline void bind_host(HostScene* H) {
     H->k.mat = H->mat.data();
     H->k.light_tri = H->light_tri.data();
     H->k.light_cum = H->light_cum.data();
+    H->k.kd = H->kd.data();
 }
 
 // first band row >= row_begin with iy % step == phase, and the band's row count

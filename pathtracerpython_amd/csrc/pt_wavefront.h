@@ -222,8 +222,8 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
         else kk = kn / q;
     }
     sp.put3(kSpNd, nd);
-    const F3 o32 = to_f3(P - ld3(S.center));      // the BVH's frame (the walks)
-    const F3 o32u = to_f3(P - ld3(S.center_s));   // the uniform units' frame
+    const F3 o32 = to_f3(P - ld3(S.kd + kKdCenter));      // the BVH's frame (the walks)
+    const F3 o32u = to_f3(P - ld3(S.kd + kKdCenterS));   // the uniform units' frame
     const F3 n32 = to_f3(unit(nd));
     ClosestAcc ca = closest_init();
     const bool any_trace = PT_WAVE_ANY(trace);
@@ -272,7 +272,7 @@ PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfS
         const int tri0 = closest_finish<false, false, true>(S, wf_get_acc(*pq), ld3(S.eye), unit(d0),
                                                             &P0, nullptr);
         if (tri0 < 0 || tri0 >= S.n_obj_tri) {   // primary ray escapes or hits the light
-            const D3 v = tri0 < 0 ? d3(0, 0, 0) : ld3(S.light_rgb);
+            const D3 v = tri0 < 0 ? d3(0, 0, 0) : ld3(S.kd + kKdLightRgb);
             D3 acc = d3(0, 0, 0);
             for (int i = 0; i < J.n_samples; ++i) acc = acc + v;
             W->acc[0] = acc.x; W->acc[1] = acc.y; W->acc[2] = acc.z;
@@ -316,7 +316,7 @@ PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfS
         if (tn < 0) {
             done = true;
         } else if (tn >= S.n_obj_tri) {   // light: main.py:214-215
-            acc = acc + ld3(S.light_rgb) * k;
+            acc = acc + ld3(S.kd + kKdLightRgb) * k;
             done = true;
         } else {
             tri = tn;
