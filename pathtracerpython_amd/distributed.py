@@ -195,6 +195,11 @@ class HostFrame:
         self.bytes = self.HEADER + slots * self.frame_bytes
         self.path = os.path.join("/dev/shm", name)
         self.owner = create
+        if create:   # a tmpfs too small for the frame would SIGBUS on first touch
+            st = os.statvfs("/dev/shm")
+            if st.f_bavail * st.f_frsize < self.bytes:
+                raise OSError(f"/dev/shm has {st.f_bavail * st.f_frsize} B free, the host frame "
+                              f"needs {self.bytes} B")
         flags = os.O_RDWR | (os.O_CREAT | os.O_EXCL if create else 0)
         fd = os.open(self.path, flags, 0o600)
         try:
