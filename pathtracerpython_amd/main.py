@@ -7,7 +7,9 @@ Same positional scene argument and flags (-r spp, -b bounces, --out,
 --show-img); the whole spp x bounce loop runs on the GPU (render.py).  Extra
 flags of this build: --seed (RNG key; default the SDL `seed`), --rr
 (Russian roulette), --size W H (override the SDL size), --devices N (N GPUs:
-one rank process per GPU, rows interleaved, one RCCL gather; launch.py).  The
+one rank process per GPU, rows interleaved, one RCCL gather; launch.py),
+--chunk-spp K [--checkpoint F] (the samples in launches of K, resumable from
+F; progressive.py).  The
 reference's interactive 3-D viewer flags (--show-scene, --show-normals,
 --show-screen, --show-inter -> plot.py) are accepted and ignored with a
 notice: the pyqtgraph viewer is out of scope.
@@ -37,6 +39,11 @@ def setup(argv=None):
     parser.add_argument('--devices', type=int, default=1,
                         help='GPUs: one rank process each (torch.distributed over RCCL); '
                              'started here unless already under torch.distributed.run')
+    parser.add_argument('--chunk-spp', type=int, default=None,
+                        help='render the -r samples in launches of this many (progressive.py)')
+    parser.add_argument('--checkpoint', default=None,
+                        help='with --chunk-spp: .npz written after every chunk; a rerun '
+                             'resumes from it')
     return parser.parse_args(argv)
 
 
@@ -110,16 +117,33 @@ def main(argv=None):
         if rank != 0:
             return None
         return finish(args, arr, fb)
+    if args.checkpoint and not args.chunk_spp:
+        raise SystemExit('--checkpoint needs --chunk-spp')
+    if args.chunk_spp and world > 1:
+        raise SystemExit('--chunk-spp runs on one device')
     with Renderer(scene) as r:
-        if W == H:   # make_image on the device (utils.py:150-161)
+        chunks = []
+        if args.chunk_spp:   # chunked, resumable (progressive.py)
+            from .progressive import render_progressive
+            from .render import image_u8
+
+            def progress(d, n):
+                chunks.append(d)
+                print(f'samples {d}/{n}', flush=True)
+            fb = render_progressive(r, W, H, args.n_rays, args.n_bounces, args.seed, args.rr,
+                                    chunk_spp=args.chunk_spp, checkpoint=args.checkpoint,
+                                    on_chunk=progress)
+            arr = image_u8(fb) if W == H else None
+        elif W == H:   # make_image on the device (utils.py:150-161)
             arr, fb = r.render_image(W, H, spp=args.n_rays, bounces=args.n_bounces,
                                      seed=args.seed, rr=args.rr, return_fb=True)
         else:        # the reference's placement for W != H (utils.py:154-156), on the host
             fb = r.render(W, H, spp=args.n_rays, bounces=args.n_bounces, seed=args.seed,
                           rr=args.rr)
             arr = None
-        print(f'render: {W}x{H}, {args.n_rays} spp, {args.n_bounces} bounces, '
-              f'kernel {r.last_kernel_ms():.3f} ms')
+        last = f'kernel {r.last_kernel_ms():.3f} ms' if chunks or not args.chunk_spp \
+            else 'all samples from the checkpoint'
+        print(f'render: {W}x{H}, {args.n_rays} spp, {args.n_bounces} bounces, {last}')
     return finish(args, arr, fb)
 
 

@@ -262,6 +262,20 @@ def test_sample_split_linearity(R):
     assert np.abs((a + b) / 2 - full).max() <= 1e-14
 
 
+def test_progressive_chunks_and_resume(R, tmp_path):
+    """progressive.py: 10 spp as chunks of 4 (sample_begin 0, 4, 8) equals
+    the one-launch frame to the sum reordering; an interrupted run resumed
+    from its checkpoint is bit-identical to the uninterrupted chunked run."""
+    from pathtracerpython_amd.progressive import render_progressive
+    full = R.render(64, 64, 10, 4, 6, out_f64=True)
+    fb = render_progressive(R, 64, 64, 10, 4, 6, chunk_spp=4)
+    assert np.abs(fb - full).max() <= 1e-14
+    ck = tmp_path / "k.npz"
+    assert render_progressive(R, 64, 64, 10, 4, 6, chunk_spp=4, checkpoint=ck,
+                              max_chunks=2) is None
+    assert np.array_equal(render_progressive(R, 64, 64, 10, 4, 6, chunk_spp=4, checkpoint=ck), fb)
+
+
 def test_random_mesh_scene(tmp_path):
     sc = random_scene(tmp_path, 300, 21)
     pk = pack_scene(sc)

@@ -93,3 +93,13 @@ def test_cli_png_matches_reference(tmp_path):
               "--seed", str(seed), "--save-raw", str(raw)])
     assert np.array_equal(np.asarray(Image.open(out)), g["png"])
     assert np.load(raw).shape == (H, W, 3)
+    # --chunk-spp 1 --checkpoint: the same frame (sample sums reordered: ~1e-16),
+    # resumable; a rerun with the finished checkpoint renders nothing more
+    raw2, ck = tmp_path / "fb2.npy", tmp_path / "ck.npz"
+    args = [CORNELL, "-r", str(spp), "-b", str(B), "--size", str(W), str(H), "--seed", str(seed),
+            "--save-raw", str(raw2), "--chunk-spp", "1", "--checkpoint", str(ck)]
+    cli.main(args)
+    assert np.abs(np.load(raw2) - np.load(raw)).max() <= 1e-14
+    assert ck.exists()
+    cli.main(args)
+    assert np.abs(np.load(raw2) - np.load(raw)).max() <= 1e-14
