@@ -11,4 +11,5 @@ and there is no CPU fallback.
 """
 from .scene_reader import Obj, Scene  # noqa: F401
 from .render import Renderer, from_list_order, render, to_list_order  # noqa: F401
+from .progressive import Checkpoint, render_progressive  # noqa: F401
 from .utils import framebuffer_to_image, make_image, make_rays, make_screen_pts  # noqa: F401
