@@ -8,6 +8,8 @@ seed + s, so a slot that rotated wrongly shows the wrong image.
             flag by a host store (the shared-memory protocol without a GPU)
   mode gpu: the band is rendered straight into the frame on cuda:0
             (HostFrame.render: out_row_stride, pt_signal), lanes_per_pixel 4
+Optional argv[9] / argv[10]: frame slots (default 2) / rank 0's wait
+timeout in s (default 60).
 Rank 0 saves the frames, (steps, H, W, 3) float32, to argv[1]."""
 import ctypes as C
 import os
@@ -27,15 +29,18 @@ from pathtracerpython_amd.launch import pg_timeout, rank_env  # noqa: E402
 def main():
     out, W, H, spp, B, seed, steps = sys.argv[1], *map(int, sys.argv[2:8])
     mode = sys.argv[8]
+    slots = int(sys.argv[9]) if len(sys.argv) > 9 else 2
+    wait_s = float(sys.argv[10]) if len(sys.argv) > 10 else 60.0
     rank, local, world = rank_env()
     dist.init_process_group("gloo", timeout=pg_timeout())
     name = [HostFrame.new_name() if rank == 0 else None]
     dist.broadcast_object_list(name, src=0)
     if rank == 0:
-        hf = HostFrame(H, W, world, rank, name[0], create=True, map_device=(mode == "gpu"))
+        hf = HostFrame(H, W, world, rank, name[0], slots=slots, create=True,
+                       map_device=(mode == "gpu"))
     dist.barrier()
     if rank != 0:
-        hf = HostFrame(H, W, world, rank, name[0], map_device=(mode == "gpu"))
+        hf = HostFrame(H, W, world, rank, name[0], slots=slots, map_device=(mode == "gpu"))
     scene_reader.VERBOSE = False
     sc = scene_reader.Scene(os.path.join(ROOT, "scenes", "cornell", "cornellroom.sdl"))
     frames = []
@@ -54,7 +59,7 @@ def main():
     def publish(step):   # this rank's band of `step` into the frame, then its flag
         if mode == "gpu":
             p = r.params(W, H, spp, B, seed + step, row_step=world, row_phase=rank, lanes_per_pixel=4)
-            hf.render(r, p, step, s, timeout_s=60)
+            hf.render(r, p, step, s, timeout_s=wait_s)
             return
         need = step - hf.slots + 1   # as HostFrame.render: the slot's last user released
         if need > 0:
@@ -74,7 +79,7 @@ def main():
         for step in range(steps):
             if step + 1 < steps:
                 publish(step + 1)
-            frames.append(hf.wait(step, timeout_s=60).copy())
+            frames.append(hf.wait(step, timeout_s=wait_s).copy())
             hf.release(step)
     else:
         for step in range(steps):

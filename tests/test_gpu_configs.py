@@ -99,6 +99,45 @@ def test_k4_band_full(R, packed):
     check_oracle(packed, lambda iy: fb[pos[iy]], W, H, 4096, 4, picks)
 
 
+@pytest.mark.timeout(400)
+def test_k4_full_frame_two_rank_processes(R, packed, tmp_path):
+    """K4 whole: Cornell 4096x4096, 4096 spp, 4 bounces through bench.py's
+    transport — two rank processes on device 0 (gloo rendezvous) render
+    their interleaved halves straight into one shared page-locked host frame
+    (distributed.HostFrame), rank 0 collects it.  With lanes_per_pixel fixed
+    any band split gives the same pixels, so the frame's rows iy % 8 == 3
+    must equal a one-process render of the 8-GPU split's band 3 bit for bit.
+    Also: every pixel finite and non-negative; the oracle on image rows 0
+    and 4095 in full (2 x 4,096 pixels x 4,096 spp) and 4 pixels on each of
+    rows 8..15 (every band of the 8-way split), to the f32 rounding of the
+    stored frame."""
+    import os
+    from conftest import ROOT
+    from pathtracerpython_amd.launch import spawn_ranks
+    W = H = 4096
+    spp, B, seed = 4096, 4, 9
+    out = str(tmp_path / "k4.npy")
+    rc = spawn_ranks(2, [os.path.join(ROOT, "tests", "rank_worker_hostframe.py"), out, str(W), str(H),
+                         str(spp), str(B), str(seed), "1", "gpu", "1", "300"])
+    assert rc == 0
+    fr = np.load(out, mmap_mode="r")[0]
+    assert fr.shape == (H, W, 3) and fr.dtype == np.float32
+    for j in range(0, H, 512):   # in slabs: finite, non-negative, lit
+        slab = np.asarray(fr[j:j + 512])
+        assert np.isfinite(slab).all() and (slab >= 0).all() and slab.mean() > 0, j
+    band3 = R.render_params(R.params(W, H, spp, B, seed, row_step=8, row_phase=3, lanes_per_pixel=4))
+    rows3 = list(range(3, H, 8))[::-1]          # band order, top first
+    assert band3.dtype == np.float32
+    assert np.array_equal(np.asarray(fr[[H - 1 - iy for iy in rows3]]), band3)
+    picks = [(ix, iy) for iy in (0, H - 1) for ix in range(W)]
+    picks += spread_pixels(W, list(range(8, 16)), 4, 5)
+    pix = np.array([ix * H + iy for ix, iy in picks], dtype=np.int64)
+    ref, _ = oracle.render(packed, W, H, spp, B, seed, pixels=pix)
+    got = np.array([fr[H - 1 - iy, ix] for ix, iy in picks], dtype=np.float64)
+    # the frame stores the f64 radiance rounded to f32 (<= 2^-24 relative)
+    assert (np.abs(got - ref) <= 2.0 ** -23 * np.abs(ref) + TOL).all()
+
+
 def test_bands_assemble_when_lane_cap_binds(R):
     """At 1024^2 x 512 spp every launch runs the lane cap (64 lanes per
     pixel), the full frame and each band of a 2-way interleave alike, so the
