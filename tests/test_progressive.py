@@ -107,3 +107,12 @@ def test_bad_arguments():
         render_progressive(FakeRenderer(), 2, 2, spp=0)
     with pytest.raises(ValueError):
         render_progressive(FakeRenderer(), 2, 2, spp=4, chunk_spp=0)
+
+
+def test_cli_checkpoint_needs_chunks(tmp_path):
+    """main.py: --checkpoint without --chunk-spp is refused before any
+    device work."""
+    from conftest import CORNELL
+    from pathtracerpython_amd import main as cli
+    with pytest.raises(SystemExit, match="--chunk-spp"):
+        cli.main([CORNELL, "-r", "2", "--checkpoint", str(tmp_path / "x.npz")])
