@@ -107,7 +107,7 @@ def test_k4_full_frame_two_rank_processes(R, packed, tmp_path):
     (distributed.HostFrame), rank 0 collects it.  With lanes_per_pixel fixed
     any band split gives the same pixels, so the frame's rows iy % 8 == 3
     must equal a one-process render of the 8-GPU split's band 3 bit for bit.
-    Also: every pixel finite and non-negative; the oracle on image rows 0
+    Also: every pixel finite; the oracle on image rows 0
     and 4095 in full (2 x 4,096 pixels x 4,096 spp) and 4 pixels on each of
     rows 8..15 (every band of the 8-way split), to the f32 rounding of the
     stored frame."""
@@ -122,9 +122,9 @@ def test_k4_full_frame_two_rank_processes(R, packed, tmp_path):
     assert rc == 0
     fr = np.load(out, mmap_mode="r")[0]
     assert fr.shape == (H, W, 3) and fr.dtype == np.float32
-    for j in range(0, H, 512):   # in slabs: finite, non-negative, lit
-        slab = np.asarray(fr[j:j + 512])
-        assert np.isfinite(slab).all() and (slab >= 0).all() and slab.mean() > 0, j
+    for j in range(0, H, 512):   # in slabs: finite and lit (a pixel may be negative:
+        slab = np.asarray(fr[j:j + 512])   # the reference's (e.r)^n with odd n, main.py:263-264)
+        assert np.isfinite(slab).all() and slab.mean() > 0, j
     band3 = R.render_params(R.params(W, H, spp, B, seed, row_step=8, row_phase=3, lanes_per_pixel=4))
     rows3 = list(range(3, H, 8))[::-1]          # band order, top first
     assert band3.dtype == np.float32
