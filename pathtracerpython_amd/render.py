@@ -174,10 +174,20 @@ class Renderer:
             pass
 
 
-def render(scene, width=None, height=None, spp=1, bounces=1, seed=None, rr=False, rr_depth=3):
-    """main.py's render as a function: framebuffer (H, W, 3) float32."""
-    with Renderer(scene) as r:
-        return r.render(width, height, spp, bounces, seed, rr, rr_depth)
+def render(scene, width=None, height=None, spp=1, bounces=1, seed=None, rr=False, rr_depth=3,
+           devices=1):
+    """main.py's render as a function: framebuffer (H, W, 3) float32.
+    devices: GPUs of this process — a count (devices 0..n-1) or a list of
+    device ids; more than one renders interleaved row bands concurrently
+    (MultiRenderer, pt_render_multi)."""
+    ids = list(range(int(devices))) if isinstance(devices, int) else [int(d) for d in devices]
+    if not ids:
+        raise ValueError("devices: need at least one")
+    if len(ids) == 1 and isinstance(devices, int):
+        with Renderer(scene) as r:
+            return r.render(width, height, spp, bounces, seed, rr, rr_depth)
+    with MultiRenderer(scene, ids) as m:
+        return m.render(width, height, spp, bounces, seed, rr, rr_depth)
 
 
 class MultiRenderer:

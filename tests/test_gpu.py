@@ -497,6 +497,16 @@ def test_from_list_order_matches_golden_png(R):
 
 
 # ------------------------------------------- one-process multi-device --
+def test_render_function_devices(cornell):
+    """render(..., devices=[0, 0]): the module-level render over several
+    handles (pt_render_multi) gives render()'s frame (at the lane cap: bit
+    for bit)."""
+    from pathtracerpython_amd.render import render
+    one = render(cornell, 40, 30, 16, 3, 5)
+    assert np.array_equal(render(cornell, 40, 30, 16, 3, 5, devices=[0, 0]), one)
+    assert np.array_equal(render(cornell, 40, 30, 16, 3, 5, devices=[0]), one)
+
+
 def test_render_multi_bands_bitwise(cornell):
     """pt_render_multi deals the rows out interleaved over its handles and
     copies each band into its rows of the host frame: bit-identical to one

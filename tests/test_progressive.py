@@ -116,3 +116,11 @@ def test_cli_checkpoint_needs_chunks(tmp_path):
     from pathtracerpython_amd import main as cli
     with pytest.raises(SystemExit, match="--chunk-spp"):
         cli.main([CORNELL, "-r", "2", "--checkpoint", str(tmp_path / "x.npz")])
+
+
+def test_render_devices_validation(cornell):
+    from pathtracerpython_amd.render import render
+    with pytest.raises(ValueError, match="devices"):
+        render(cornell, 4, 4, devices=0)
+    with pytest.raises(ValueError, match="devices"):
+        render(cornell, 4, 4, devices=[])
