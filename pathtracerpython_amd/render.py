@@ -13,6 +13,7 @@ radiance of the reference's pixel k = ix*H + iy (utils.py:64-69), before
 make_image's min-max normalisation.
 """
 import ctypes as C
+import numbers
 
 import numpy as np
 
@@ -180,10 +181,11 @@ def render(scene, width=None, height=None, spp=1, bounces=1, seed=None, rr=False
     devices: GPUs of this process — a count (devices 0..n-1) or a list of
     device ids; more than one renders interleaved row bands concurrently
     (MultiRenderer, pt_render_multi)."""
-    ids = list(range(int(devices))) if isinstance(devices, int) else [int(d) for d in devices]
+    count = isinstance(devices, numbers.Integral)
+    ids = list(range(int(devices))) if count else [int(d) for d in devices]
     if not ids:
         raise ValueError("devices: need at least one")
-    if len(ids) == 1 and isinstance(devices, int):
+    if len(ids) == 1 and count:
         with Renderer(scene) as r:
             return r.render(width, height, spp, bounces, seed, rr, rr_depth)
     with MultiRenderer(scene, ids) as m:

@@ -124,3 +124,5 @@ def test_render_devices_validation(cornell):
         render(cornell, 4, 4, devices=0)
     with pytest.raises(ValueError, match="devices"):
         render(cornell, 4, 4, devices=[])
+    with pytest.raises(ValueError, match="devices"):
+        render(cornell, 4, 4, devices=np.int64(0))
