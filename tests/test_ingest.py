@@ -166,3 +166,50 @@ def test_k5_generator_ingests_identically(tmp_path, quiet):
     assert a.n_tri == 4000 + 10 + 2 and a.n_obj == 6
     for k in ("tri_v", "tri_n", "tri_area", "tri_obj"):
         assert getattr(a, k).tobytes() == getattr(b, k).tobytes(), k
+
+
+@pytest.mark.parametrize("chunk", ["24", "1000000"])
+@pytest.mark.parametrize("text,exc", [
+    # the first error in file order wins, whichever chunk finds it
+    ("v 0 0 0\nv 1 0 0\nv 2 0 0\nf 1 2 3\n" + "v 0 1 0\n" * 40 + "f 1/1 2 3\n", ZeroDivisionError),
+    ("v 0 0 0\nv 1 0 0\nf 1/1 2 3\n" + "v 0 1 0\n" * 40 + "v 2 0 0\nf 1 2 43\n", ValueError),
+    ("v 0 0 0\nv 1 0 0\nv 0 1 0\n" + "f 1 2 3\n" * 30 + "f 1 2 99\n" + "v 5 5 5\n" * 80, IndexError),
+    ("v 0 0 0\n" * 3 + "v 1 0 0\nv 0 1 0\n" + "f -1 -2 -3\n" * 20 + "v 9 9 x\n", ValueError),
+])
+def test_chunked_parse_reports_the_first_error(tmp_path, quiet, monkeypatch, chunk, text, exc):
+    """The native reader's chunks (PT_INGEST_CHUNK bytes; 24: one to two
+    lines each) raise the error the serial reader meets first."""
+    monkeypatch.setenv("PT_INGEST_CHUNK", chunk)
+    p = tmp_path / "bad.obj"
+    p.write_text(text)
+    with pytest.raises(exc):
+        _read(p, True)
+    with pytest.raises(exc):
+        _read(p, False)
+
+
+def test_chunked_parse_equals_serial(tmp_path, quiet, monkeypatch):
+    """Many small chunks on several threads give the one-chunk result bit for
+    bit (negative indices reaching back across chunk boundaries included)."""
+    rs = np.random.RandomState(5)
+    lines = []
+    nv = 0
+    for i in range(3000):
+        if rs.rand() < 0.5 or nv < 4:
+            lines.append("v %.17g %.17g %.17g" % tuple(rs.normal(0, 1, 3)))
+            nv += 1
+        elif rs.rand() < 0.5:
+            lines.append("f %d %d %d" % tuple(rs.choice(nv, 3, replace=False) + 1))
+        else:
+            lines.append("f %d %d %d %d" % tuple(-(rs.choice(nv, 4, replace=False) + 1)))
+        if rs.rand() < 0.05:
+            lines.append("vn 0 0 1  # skipped")
+    p = tmp_path / "mix.obj"
+    p.write_text("\r\n".join(lines) + "\r\n")
+    monkeypatch.setenv("PT_INGEST_CHUNK", "1000000")
+    one = _read(p, True)
+    monkeypatch.setenv("PT_INGEST_CHUNK", "50")
+    many = _read(p, True)
+    assert one.arrays is not None and many.arrays is not None
+    _same(one, many)
+    _same(many, _read(p, False))
