@@ -206,6 +206,10 @@ class HostFrame:
             if create:
                 os.ftruncate(fd, self.bytes)
             self._mm = mmap.mmap(fd, self.bytes, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        except BaseException:
+            if create:   # no half-made frame left in /dev/shm
+                os.unlink(self.path)
+            raise
         finally:
             os.close(fd)
         self._cbuf = C.c_char.from_buffer(self._mm)
