@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 5
+#define PT_API_VERSION 6
 
 /* error codes */
 #define PT_OK 0
@@ -145,6 +145,11 @@ typedef struct pt_scene pt_scene;
 
 int pt_api_version(void);
 const char* pt_last_error(void);
+/* Content hash (16 hex digits) of the sources the library was compiled from
+ * (the .h and .hip files of csrc/ and this header; pathtracerpython_amd/build.py).  The
+ * Python binding refuses a library whose id is not the hash of the sources on
+ * disk, and measurements name the loaded library's id.  (v6) */
+const char* pt_build_id(void);
 
 /* number of HIP devices visible to the library */
 int pt_device_count(int32_t* count);
@@ -285,6 +290,11 @@ typedef struct pt_mesh {
 } pt_mesh;
 int pt_obj_load(const char* path, pt_mesh** out);
 void pt_mesh_free(pt_mesh* mesh);
+
+/* Test hook (v6): the next pt_render_multi calls fail with PT_EHIP while
+ * dealing band `multi_band`, after bands 0..multi_band-1 were launched (the
+ * error path's drain); -1 (the default) turns it off.  Process-wide. */
+int pt_test_fault_inject(int32_t multi_band);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,7 @@
 """ctypes mirror of include/pt_capi.h (structs, flags, error codes)."""
 import ctypes as C
 
-PT_API_VERSION = 5
+PT_API_VERSION = 6
 
 PT_OK = 0
 PT_EINVAL = -1

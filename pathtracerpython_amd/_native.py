@@ -26,6 +26,8 @@ def _bind(lib):
     sig = {
         "pt_api_version": ([], C.c_int),
         "pt_last_error": ([], C.c_char_p),
+        "pt_build_id": ([], C.c_char_p),
+        "pt_test_fault_inject": ([C.c_int32], C.c_int),
         "pt_device_count": ([ip], C.c_int),
         "pt_scene_create": ([C.POINTER(PtSceneDesc), C.POINTER(vp)], C.c_int),
         "pt_scene_create_on": ([C.POINTER(PtSceneDesc), C.c_int32, C.POINTER(vp)], C.c_int),
@@ -56,7 +58,8 @@ def _bind(lib):
     return lib
 
 
-EXPORTS = ("pt_api_version", "pt_last_error", "pt_device_count", "pt_scene_create",
+EXPORTS = ("pt_api_version", "pt_last_error", "pt_build_id", "pt_test_fault_inject",
+           "pt_device_count", "pt_scene_create",
            "pt_scene_create_on", "pt_render_multi", "pt_scene_destroy", "pt_band_rows",
            "pt_render_device", "pt_render", "pt_last_kernel_ms", "pt_intersect_objects", "pt_compute_color",
            "pt_image_u8_device", "pt_image_u8", "pt_assemble_bands_device", "pt_host_map",
@@ -77,13 +80,33 @@ def lib():
         import torch  # noqa: F401  (shares libamdhip64 with torch)
     except Exception:
         pass
-    lib_ = _bind(C.CDLL(LIB_PATH))
+    raw = C.CDLL(LIB_PATH)
     from ._abi import PT_API_VERSION
-    if lib_.pt_api_version() != PT_API_VERSION:
-        raise NativeError(f"{LIB_PATH} has C-ABI version {lib_.pt_api_version()}, this binding "
+    if not hasattr(raw, "pt_build_id") or raw.pt_api_version() != PT_API_VERSION:
+        raise NativeError(f"{LIB_PATH} has C-ABI version {raw.pt_api_version()}, this binding "
                           f"needs {PT_API_VERSION}: rebuild it (python __graft_entry__.py build)")
+    lib_ = _bind(raw)
+    got = lib_.pt_build_id().decode("ascii", "replace")
+    want = source_sha()
+    # a library built from other sources than those on disk is refused, so a
+    # measurement never carries the wrong sources' name (build.py); dev
+    # variants built from patched sources opt out explicitly and are still
+    # named by their own id (bench.py reports build_id())
+    if got != want and os.environ.get("PT_ALLOW_FOREIGN_BUILD") != "1":
+        raise NativeError(f"{LIB_PATH} was built from sources {got}, the sources on disk are {want}: "
+                          "rebuild it (python __graft_entry__.py build)")
     _lib = lib_
     return _lib
+
+
+def source_sha():
+    from .build import source_sha as sha
+    return sha()
+
+
+def build_id():
+    """The loaded library's PT_BUILD_ID (the content hash of its sources)."""
+    return lib().pt_build_id().decode("ascii", "replace")
 
 
 def last_error():

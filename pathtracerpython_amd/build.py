@@ -1,5 +1,13 @@
 """Build libpt_hip.so in-tree with hipcc for gfx950 (no JIT cache: the built
-library travels with the repository snapshot to the GPU box)."""
+library travels with the repository snapshot to the GPU box).
+
+Every build is stamped with the content hash of the sources it was compiled
+from (`source_sha`: csrc/*.h, csrc/*.hip, include/pt_capi.h), compiled in as
+PT_BUILD_ID and exported by `pt_build_id()`.  Staleness is decided by that
+hash, not by file times, and `_native.lib()` refuses a library whose id is not
+the hash of the sources on disk, so a measurement always names the sources of
+the binary that produced it (bench.py reports the loaded library's id)."""
+import hashlib
 import os
 import subprocess
 import sys
@@ -7,35 +15,73 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
+HEADER = os.path.join(ROOT, "include", "pt_capi.h")
 OUT = os.path.join(HERE, "_lib", "libpt_hip.so")
 SOURCES = ["pt_hip.hip"]
-DEPS = SOURCES + ["pt_core.h", "pt_math.h", "pt_path.h", "pt_prepare.h", "pt_image.h", "pt_ingest.h", "pt_wavefront.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # -ffp-contract=off: every f64 operation rounds separately, as the reference's
 # numpy does; the f32 filter writes its fmaf() explicitly.
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off", "-Wall"]
+# the id string in the library: MARKER followed by the 16 hex digits
+MARKER = b"PT_BUILD_ID="
+ID_LEN = 16
 
 
-def _stale():
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, f) for f in DEPS] + [os.path.join(ROOT, "include", "pt_capi.h")]
-    return any(os.path.getmtime(p) > t for p in deps)
+def source_files(csrc=CSRC, header=HEADER):
+    return [os.path.join(csrc, f) for f in sorted(os.listdir(csrc))
+            if f.endswith((".h", ".hip"))] + [header]
+
+
+def source_sha(csrc=CSRC, header=HEADER):
+    """Content hash of the kernel sources (16 hex digits)."""
+    h = hashlib.sha256()
+    for p in source_files(csrc, header):
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:ID_LEN]
+
+
+def embedded_build_id(path):
+    """The PT_BUILD_ID a built library carries, read from its bytes (no load,
+    no HIP runtime), or None."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(MARKER)
+    if i < 0:
+        return None
+    s = data[i + len(MARKER):i + len(MARKER) + ID_LEN]
+    return s.decode("ascii", "replace")
+
+
+def _stale(out=OUT, csrc=CSRC):
+    return embedded_build_id(out) != source_sha(csrc)
+
+
+def compile_lib(out, defines=(), csrc=CSRC, verbose=True):
+    """hipcc the library into `out`, stamped with the hash of `csrc`'s sources
+    (dev variants pass -D switches; they carry the same id when built from the
+    same sources)."""
+    sha = source_sha(csrc)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = ([HIPCC] + FLAGS + [f"-DPT_BUILD_ID=\"{sha}\""] + ["-D" + d for d in defines] +
+           ["-o", out + ".tmp"] +
+           [os.path.join(csrc, s) for s in SOURCES])
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
 
 
 def build(force=False, verbose=True):
     if not force and not _stale():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    return compile_lib(OUT, verbose=verbose)
 
 
 if __name__ == "__main__":

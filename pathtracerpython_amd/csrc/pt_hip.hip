@@ -777,6 +777,22 @@ extern "C" {
 
 int pt_api_version(void) { return PT_API_VERSION; }
 
+// The content hash of the sources this library was compiled from
+// (pathtracerpython_amd/build.py passes it as PT_BUILD_ID; the marker lets the
+// build read it back from the file without loading it).
+#ifndef PT_BUILD_ID
+#error "PT_BUILD_ID (the sources' content hash) must be defined: build with pathtracerpython_amd/build.py"
+#endif
+static const char pt_build_id_str[] = "PT_BUILD_ID=" PT_BUILD_ID;
+const char* pt_build_id(void) { return pt_build_id_str + 12; }
+
+// test hook (tests/test_gpu.py): pt_render_multi fails while dealing band i
+static std::atomic<int32_t> g_fault_multi{-1};
+int pt_test_fault_inject(int32_t multi_band) {
+    g_fault_multi.store(multi_band);
+    return PT_OK;
+}
+
 const char* pt_last_error(void) { return g_err.c_str(); }
 
 int pt_device_count(int32_t* count) {
@@ -1360,11 +1376,9 @@ int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* 
     }
     int rc = validate(p);
     if (rc) return rc;
-    // fault injection for the tests of the error path (tests/test_gpu.py):
-    // PT_FAULT_INJECT_MULTI=i makes dealing band i fail after bands 0..i-1
-    // were launched
-    const char* fi = getenv("PT_FAULT_INJECT_MULTI");
-    const int32_t fail_at = fi ? (int32_t)atoi(fi) : -1;
+    // fault injection for the tests of the error path (pt_test_fault_inject):
+    // dealing band i fails after bands 0..i-1 were launched
+    const int32_t fail_at = g_fault_multi.load();
     if (p->row_step != 1) return fail(PT_EINVAL, "pt_render_multi deals out the rows itself: row_step must be 1");
     if (p->out_row_stride != 0) return fail(PT_EINVAL, "pt_render_multi writes the packed layout: out_row_stride must be 0");
     int32_t first = 0, total = 0;
@@ -1410,7 +1424,7 @@ int pt_render_multi(pt_scene* const* scenes, int32_t n, const pt_render_params* 
                         s->out_cap = bytes;
                 }
             }
-            if (rci == PT_OK && i == fail_at) rci = fail(PT_EHIP, "fault injected (PT_FAULT_INJECT_MULTI)");
+            if (rci == PT_OK && i == fail_at) rci = fail(PT_EHIP, "fault injected (pt_test_fault_inject)");
             if (rci == PT_OK) {
                 pt_stats st;
                 rci = pt_render_device(s, &bp[i], s->out_dev, s->stream, (count && stats) ? &st : nullptr);

@@ -132,22 +132,48 @@ def render_distributed(renderer, width, height, spp=1, bounces=1, seed=None, rr=
     if transport == "host":
         if return_tiles:
             raise ValueError("return_tiles needs the device transport")
+        from ._native import NativeError
         name = [HostFrame.new_name() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(name, src=0, group=group)
-        hf = HostFrame(height, width, world, rank, name[0], create=True) if rank == 0 else None
+
+        def agree(err):
+            """Every rank learns the first rank's error (or None) before any
+            rank renders or waits, so no rank is left in a barrier or rank 0
+            spinning on a flag that never comes."""
+            if world == 1:
+                return err
+            errs = [None] * world
+            dist.all_gather_object(errs, err, group=group)
+            return next((e for e in errs if e), None)
+
+        def attempt(fn):
+            try:
+                return fn(), None
+            except Exception as e:   # noqa: BLE001 (re-raised on every rank)
+                return None, f"rank {rank}: {type(e).__name__}: {e}"
+        hf, err = (attempt(lambda: HostFrame(height, width, world, rank, name[0], create=True))
+                   if rank == 0 else (None, None))
         if world > 1:
-            dist.barrier(group=group)
-            if rank != 0:
-                hf = HostFrame(height, width, world, rank, name[0])
+            # rank 0's file exists (or its error is known) before the others open it
+            first = agree(err)
+            if first is None and rank != 0:
+                hf, err = attempt(lambda: HostFrame(height, width, world, rank, name[0]))
+            err = first or agree(err)
         try:
-            hf.render(renderer, p, 0, torch.cuda.current_stream().cuda_stream)
+            if err:
+                raise NativeError(f"host frame: {err}")
+            _, err = attempt(lambda: hf.render(renderer, p, 0, torch.cuda.current_stream().cuda_stream))
+            err = agree(err)
+            if err:
+                raise NativeError(f"host frame render: {err}")
             fb = hf.wait(0).copy() if rank == 0 else None
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier(group=group)
         finally:
-            hf.close()
+            if hf is not None:
+                hf.close()
         return fb
     if transport != "device":
         raise ValueError(f"transport must be 'device' or 'host', not {transport!r}")
@@ -216,6 +242,7 @@ class HostFrame:
         self.host = C.addressof(self._cbuf)
         self._lib = _native.lib()
         self.dev = None
+        self._rendered = False
         if map_device:
             dev = C.c_void_p()
             rc = self._lib.pt_host_map(C.c_void_p(self.host), self.bytes, C.byref(dev))
@@ -270,6 +297,7 @@ class HostFrame:
             renderer.render_device(with_flags(p, out_row_stride=stride), ptr, stream)
         if events:
             events[1].record()
+        self._rendered = True
         _native.check(self._lib.pt_signal(C.c_void_p(self.dev + self.READY + 64 * self.rank),
                                           step + 1, C.c_void_p(stream or 0)), "pt_signal")
 
@@ -289,6 +317,11 @@ class HostFrame:
             return
         from . import _native
         if self.dev is not None:
+            if self._rendered:
+                # renders into the frame may still be running (an error
+                # between render() and wait()): unmap only after they finish
+                import torch
+                torch.cuda.synchronize()
             self.dev = None
             _native.check(self._lib.pt_host_unmap(C.c_void_p(self.host)), "pt_host_unmap")
         self.u64 = None

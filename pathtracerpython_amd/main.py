@@ -93,8 +93,17 @@ def render_ranks(scene, args, W, H):
         dist.destroy_process_group()
 
 
+def check_args(args):
+    """Reject flag combinations before any rank process starts."""
+    if args.checkpoint and not args.chunk_spp:
+        raise SystemExit('--checkpoint needs --chunk-spp')
+    if args.chunk_spp and args.devices > 1:
+        raise SystemExit('--chunk-spp runs on one device (--devices 1)')
+
+
 def main(argv=None):
     args = setup(argv)
+    check_args(args)
     from .launch import rank_env, spawn_ranks, under_launcher
     if args.devices > 1 and not under_launcher():
         # one fresh process per GPU; this parent never touches the GPU
@@ -117,10 +126,6 @@ def main(argv=None):
         if rank != 0:
             return None
         return finish(args, arr, fb)
-    if args.checkpoint and not args.chunk_spp:
-        raise SystemExit('--checkpoint needs --chunk-spp')
-    if args.chunk_spp and world > 1:
-        raise SystemExit('--chunk-spp runs on one device')
     with Renderer(scene) as r:
         chunks = []
         if args.chunk_spp:   # chunked, resumable (progressive.py)

@@ -33,7 +33,8 @@ pmc() {   # pmc NAME "COUNTERS" driver args...
 # 1-2. K2 counters (3 launches each)
 pmc k2_fetch FETCH_SIZE "$R/scripts/prof_k2.py" 3
 pmc k2_write WRITE_SIZE "$R/scripts/prof_k2.py" 3
-python3 "$R/scripts/summarize_pmc.py" "$P/${TAG}_pmc_k2_traffic.json" "$OUT/k2_fetch" "$OUT/k2_write" > /dev/null
+PMC_NOTE="algorithmic bytes: the framebuffer, 512x512x3 f32 = 3,145,728 B written" \
+    python3 "$R/scripts/summarize_pmc.py" "$P/${TAG}_pmc_k2_traffic.json" "$OUT/k2_fetch" "$OUT/k2_write" > /dev/null
 python3 "$R/scripts/stamp_traffic.py" "$P/${TAG}_pmc_k2_traffic.json" "$P/traffic_k2.json" median \
     "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), k_render<false,false,false>, 512x512 64spp 4b, median over 3 dispatches; profiles/${TAG}_pmc_k2_traffic.json; FETCH doubled (gfx950)"
 pmc k2_sq1 "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM" "$R/scripts/prof_k2.py" 2
@@ -64,12 +65,12 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 cp "$OUT/trace_k5s/k5_kernel_stats.csv" "$P/${TAG}_k5_kernel_stats_serial.csv"
 pmc k5_fetch FETCH_SIZE "$R/scripts/prof_k5.py" 1 1024 256
 pmc k5_write WRITE_SIZE "$R/scripts/prof_k5.py" 1 1024 256
-PMC_KERNEL=k_wf_shadow python3 "$R/scripts/summarize_pmc.py" "$P/${TAG}_pmc_k5_traffic.json" \
-    "$OUT/k5_fetch" "$OUT/k5_write" > /dev/null
-PMC_KERNEL=k_wf_closest python3 "$R/scripts/summarize_pmc.py" "$P/${TAG}_pmc_k5_closest_traffic.json" \
-    "$OUT/k5_fetch" "$OUT/k5_write" > /dev/null
-python3 "$R/scripts/stamp_traffic.py" "$P/${TAG}_pmc_k5_traffic.json" "$P/traffic_k5.json" mean \
-    "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), k_wf_shadow, 1024x1024 256spp 4b, mean over its dispatches; profiles/${TAG}_pmc_k5_traffic.json; FETCH doubled (gfx950)" \
+PMC_KERNEL=k_wf_shadow PMC_NOTE="k_wf_shadow (K5 one-ray shadow walks, 1024x1024 256 spp): bytes beyond L2 of the BVH node / leaf records and the shadow query records (Infinity Cache hits included)" \
+    python3 "$R/scripts/summarize_pmc.py" "$P/${TAG}_pmc_k5_traffic.json" "$OUT/k5_fetch" "$OUT/k5_write" > /dev/null
+PMC_KERNEL=k_wf_closest PMC_NOTE="k_wf_closest (K5 closest-hit walks, 1024x1024 256 spp): bytes beyond L2 of the BVH node / leaf records and the closest query records (Infinity Cache hits included)" \
+    python3 "$R/scripts/summarize_pmc.py" "$P/${TAG}_pmc_k5_closest_traffic.json" "$OUT/k5_fetch" "$OUT/k5_write" > /dev/null
+python3 "$R/scripts/stamp_traffic.py" "$P/${TAG}_pmc_k5_traffic.json" "$P/traffic_k5.json" median \
+    "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), k_wf_shadow, 1024x1024 256spp 4b, median over its dispatches; profiles/${TAG}_pmc_k5_traffic.json; FETCH doubled (gfx950)" \
     "$P/${TAG}_pmc_k5_closest_traffic.json"
 cd "$R"
 cp "$P/traffic_k5.json" "$R/profiles/traffic_k5.json"

@@ -11,13 +11,17 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-import bench  # noqa: E402
+from pathtracerpython_amd import build  # noqa: E402
 
 src, dst, stat, text = sys.argv[1:5]
 key = "hbm_bytes_per_launch_mean" if stat == "mean" else "hbm_bytes_per_launch"
 d = json.load(open(src))
-t = {"hbm_bytes_per_launch": d[key], "source_sha": bench.source_sha(), "source": text,
-     "dispatches": d.get("dispatches")}
+# the stamp is the id of the library that was measured (which _native.lib()
+# only loads when it is the hash of the sources on disk)
+sha = build.embedded_build_id(build.OUT)
+assert sha == build.source_sha(), (sha, build.source_sha())
+t = {"hbm_bytes_per_launch": d[key], "statistic": "mean" if stat == "mean" else "median",
+     "source_sha": sha, "source": text, "dispatches": d.get("dispatches")}
 if len(sys.argv) > 5:
     c = json.load(open(sys.argv[5]))
     t["closest_hbm_bytes_per_launch"] = c[key]

@@ -1,0 +1,48 @@
+"""Rank process for tests/test_bench_legs.py: the end of a bench.py job
+(bench.finish_line: the secondary frame transport, bounded and non-fatal, then
+rank 0's one line) over gloo on CPU.  The headline result is a synthetic line
+of bench.py's shape (no GPU here); the secondary leg is a gloo collective,
+as the device frame's gather is one, which PT_BENCH_INJECT_DEVICE_LEG makes
+fail or hang on a chosen rank.
+
+    python tests/bench_leg_worker.py spawn N   # the parent: N rank processes
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def rank_main():
+    import torch
+    import torch.distributed as dist
+    import bench
+    from pathtracerpython_amd.launch import pg_timeout, rank_env
+    rank, _, world = rank_env()
+    dist.init_process_group("gloo", timeout=pg_timeout())
+    result = None
+    if rank == 0:
+        result = {"metric": bench.METRIC, "value": 3052.0, "unit": "Mpath-samples/s", "n_gpus": world,
+                  "ms_per_step": 5.5, "config": {"frame": "host"},
+                  "frame_modes": {"host": {"ms_per_step": 5.5, "value": 3052.0,
+                                           "legs_ms": {"band_kernel_max": 5.49, "band_kernel_min": 5.48,
+                                                       "after_kernel": 0.01}},
+                                  "device": {"pending": "runs after the headline"}},
+                  "linf_vs_cpu_ref": 6.0e-8, "linf_checked": "all 262144 pixels"}
+
+    def leg():   # a collective across the ranks, as the RCCL gather is
+        t = torch.full((4,), float(rank + 1))
+        dist.all_reduce(t)
+        return {"ms_per_step": 5.6, "value": 3000.0, "legs_ms": {"gather": float(t[0])}}
+    budget = float(os.environ.get("PT_BENCH_LEG_TIMEOUT_S", "60"))
+    bench.finish_line(result, "device", leg, budget, rank, world, dist)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "spawn":
+        from pathtracerpython_amd.launch import spawn_ranks
+        sys.exit(spawn_ranks(int(sys.argv[2]), [os.path.abspath(__file__)]))
+    rank_main()

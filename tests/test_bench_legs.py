@@ -1,0 +1,76 @@
+"""bench.py --gpus N prints its headline line whatever the
+secondary (device-frame, RCCL-gather) leg does.  The leg runs only after rank
+0's line is complete; an exception on any rank is recorded under
+frame_modes.device, a leg that never returns is ended by a watchdog that
+prints the headline line first — one parsed JSON line, status 0, every time.
+gloo world 2 on CPU (tests/bench_leg_worker.py); the GPU suite runs the same
+injection through bench.py itself (test_gpu.py)."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from conftest import ROOT
+
+WORKER = os.path.join(ROOT, "tests", "bench_leg_worker.py")
+
+
+def run(world, inject=None, timeout_s=None):
+    env = dict(os.environ)
+    env.pop("PT_BENCH_INJECT_DEVICE_LEG", None)
+    if inject:
+        env["PT_BENCH_INJECT_DEVICE_LEG"] = inject
+    if timeout_s:
+        env["PT_BENCH_LEG_TIMEOUT_S"] = str(timeout_s)
+    t0 = time.monotonic()
+    res = subprocess.run([sys.executable, WORKER, "spawn", str(world)], env=env, capture_output=True,
+                         text=True, timeout=240)
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    return res, [json.loads(ln) for ln in lines], time.monotonic() - t0
+
+
+def check_headline(line, world):
+    assert line["n_gpus"] == world and line["value"] == 3052.0
+    assert line["frame_modes"]["host"]["legs_ms"]["band_kernel_max"] == 5.49
+    assert line["linf_vs_cpu_ref"] == 6.0e-8
+
+
+def test_secondary_leg_runs():
+    res, lines, _ = run(2)
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert len(lines) == 1
+    check_headline(lines[0], 2)
+    assert lines[0]["frame_modes"]["device"]["legs_ms"]["gather"] == 3.0   # 1 + 2 over the ranks
+
+
+@pytest.mark.parametrize("who", [0, 1])
+def test_secondary_leg_raises(who):
+    res, lines, dt = run(2, inject=f"raise:{who}")
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert len(lines) == 1
+    check_headline(lines[0], 2)
+    err = lines[0]["frame_modes"]["device"]["error"]
+    assert f"rank {who}: RuntimeError: injected device-leg failure" in err
+    assert dt < 60
+
+
+@pytest.mark.parametrize("who", [0, 1])
+def test_secondary_leg_hangs(who):
+    """The leg never returns on one rank (a collective that never completes):
+    the watchdogs end every rank after the budget, rank 0's printing the
+    headline line with the error first."""
+    res, lines, dt = run(2, inject=f"hang:{who}", timeout_s=4)
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert len(lines) == 1
+    check_headline(lines[0], 2)
+    assert "no outcome within 4 s" in lines[0]["frame_modes"]["device"]["error"]
+    assert dt < 90
+
+
+def test_line_printed_once_on_a_single_rank():
+    res, lines, _ = run(1, inject="raise:0")
+    assert res.returncode == 0 and len(lines) == 1
+    assert "rank 0: RuntimeError" in lines[0]["frame_modes"]["device"]["error"]

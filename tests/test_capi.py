@@ -45,7 +45,7 @@ def test_abi_struct_layout(hostcheck):
 
 def test_api_version():
     from pathtracerpython_amd._abi import PT_API_VERSION
-    assert _native.lib().pt_api_version() == PT_API_VERSION == 5
+    assert _native.lib().pt_api_version() == PT_API_VERSION == 6
 
 
 @pytest.mark.parametrize("H,step,phase,b,e", [(10, 1, 0, 0, 10), (10, 3, 1, 0, 10),
@@ -156,3 +156,59 @@ def test_host_map_without_gpu_fails_loudly():
     buf = np.zeros(4096, dtype=np.uint8)
     dev = C.c_void_p()
     assert _native.lib().pt_host_map(C.c_void_p(buf.ctypes.data), buf.nbytes, C.byref(dev)) == -4
+
+
+def test_build_id_is_the_sources_hash():
+    """the library carries the content hash of the sources it
+    was built from (pt_build_id, compiled in by build.py), which is the hash
+    of the sources on disk, and build.py reads the same id from the file."""
+    from pathtracerpython_amd import build
+    sha = build.source_sha()
+    assert _native.build_id() == sha
+    assert build.embedded_build_id(_native.LIB_PATH) == sha
+    assert not build._stale()
+
+
+def test_library_with_another_build_id_is_refused(tmp_path):
+    """A library stamped with another sha (here: a copy whose embedded id is
+    rewritten) is refused by _native.lib(), in a fresh process."""
+    import subprocess
+    import sys
+    from pathtracerpython_amd import build
+    data = open(_native.LIB_PATH, "rb").read()
+    i = data.find(build.MARKER)
+    assert i >= 0 and data.find(build.MARKER, i + 1) < 0
+    j = i + len(build.MARKER)
+    other = "0123456789abcdef" if data[j:j + 16] != b"0123456789abcdef" else "fedcba9876543210"
+    bad = tmp_path / "libpt_hip.so"
+    bad.write_bytes(data[:j] + other.encode() + data[j + 16:])
+    assert build.embedded_build_id(str(bad)) == other
+    code = ("from pathtracerpython_amd import _native\n"
+            "try:\n    _native.lib()\nexcept _native.NativeError as e:\n    print('REFUSED', e)\n"
+            "else:\n    print('LOADED', _native.build_id())\n")
+    env = dict(os.environ, PT_HIP_LIB=str(bad))
+    env.pop("PT_ALLOW_FOREIGN_BUILD", None)
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=120).stdout
+    assert "REFUSED" in out and f"built from sources {other}" in out, out
+    # dev variants opt out explicitly, and are then named by their own id
+    env["PT_ALLOW_FOREIGN_BUILD"] = "1"
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=120).stdout
+    assert f"LOADED {other}" in out, out
+
+
+def test_build_is_stale_when_a_source_changes(tmp_path):
+    """Staleness is the content hash, not file times: a touched but unchanged
+    source is not stale, an edited copy of the sources is."""
+    import shutil
+    from pathtracerpython_amd import build
+    os.utime(os.path.join(build.CSRC, "pt_core.h"))
+    assert not build._stale()
+    csrc = tmp_path / "csrc"
+    shutil.copytree(build.CSRC, csrc)
+    assert build.source_sha(str(csrc)) == build.source_sha()
+    with open(csrc / "pt_core.h", "a") as f:
+        f.write("\n// edit\n")
+    assert build.source_sha(str(csrc)) != build.source_sha()
+    assert build._stale(csrc=str(csrc))

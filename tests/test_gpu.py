@@ -571,20 +571,23 @@ def test_render_multi_lanes_contract(cornell):
         assert np.array_equal(m.render(W, H, 64, 4, 9, out_f64=True, lanes_per_pixel=32), ref32)
 
 
-def test_render_multi_error_drains_launched_devices(cornell, monkeypatch):
+def test_render_multi_error_drains_launched_devices(cornell):
     """a failure while dealing band i (fault injected after
-    bands 0..i-1 were launched) returns the error after draining those
-    devices; the same handles then render bit-exactly."""
+    bands 0..i-1 were launched, pt_test_fault_inject) returns the error after
+    draining those devices; the same handles then render bit-exactly."""
     from pathtracerpython_amd.render import MultiRenderer
     W = H = 256
     with Renderer(cornell) as r:
         ref = r.render_params(r.params(W, H, 64, 4, 5, lanes_per_pixel=16))
+    lib = _native.lib()
     with MultiRenderer(cornell, [0] * 4) as m:
         for i in (1, 3):
-            monkeypatch.setenv("PT_FAULT_INJECT_MULTI", str(i))
-            with pytest.raises(_native.NativeError, match=f"device {i}: fault injected"):
-                m.render(W, H, 64, 4, 5, lanes_per_pixel=16)
-            monkeypatch.delenv("PT_FAULT_INJECT_MULTI")
+            lib.pt_test_fault_inject(i)
+            try:
+                with pytest.raises(_native.NativeError, match=f"device {i}: fault injected"):
+                    m.render(W, H, 64, 4, 5, lanes_per_pixel=16)
+            finally:
+                lib.pt_test_fault_inject(-1)
             assert np.array_equal(m.render(W, H, 64, 4, 5, lanes_per_pixel=16), ref)
 
 
@@ -692,3 +695,30 @@ def test_bench_host_frame_path_two_ranks(tmp_path):
     assert line["linf_checked"] == "all 262144 pixels" and line["pixels_over"]["1e-6"] == 0
     legs = line["frame_modes"]["host"]["legs_ms"]
     assert legs["band_kernel_max"] >= legs["band_kernel_min"] > 0
+
+
+@pytest.mark.parametrize("inject", ["raise:1", "hang:1"])
+def test_bench_headline_survives_a_failing_secondary_leg(inject):
+    """VERDICT r04 #1 through bench.py itself (two rank processes on device 0,
+    PT_BENCH_REHEARSE): the secondary leg fails or never returns on rank 1,
+    and the job still prints ONE line with the host-frame headline — value,
+    legs, the whole frame against the oracle — and the leg's error, status 0."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, PT_BENCH_REHEARSE="1", PT_BENCH_INJECT_DEVICE_LEG=inject,
+               PT_BENCH_LEG_TIMEOUT_S="10")
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4",
+                          "--warmup", "1", "--no-cpu-baseline"], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [json.loads(ln) for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["config"]["frame"] == "host"
+    assert line["frame_modes"]["host"]["legs_ms"]["band_kernel_max"] > 0
+    assert line["linf_checked"] == "all 262144 pixels" and line["pixels_over"]["1e-6"] == 0
+    err = line["frame_modes"]["device"]["error"]
+    assert ("rank 1: RuntimeError: injected" in err) if inject.startswith("raise") else \
+        ("no outcome within 10 s" in err)

@@ -116,3 +116,23 @@ def test_host_frame_file_lifecycle():
     b.close()
     a.close()
     assert not os.path.exists(os.path.join("/dev/shm", name))
+
+
+@pytest.mark.parametrize("who,match", [("rank0", "rank 0: NativeError: pt_host_map failed"),
+                                       ("rank1", "rank 1: OSError: injected")])
+def test_render_distributed_host_errors(tmp_path, who, match):
+    """render_distributed(transport="host") exchanges the frame's
+    open errors before any rank renders or waits, so a failure on rank 0
+    (creation) or on another rank (open) raises the same error on every rank
+    within seconds — not a barrier or a flag wait until the timeout."""
+    import time
+    import torch
+    from pathtracerpython_amd.launch import spawn_ranks
+    if torch.cuda.is_available() and who == "rank0":
+        pytest.skip("a GPU is visible: rank 0's pt_host_map would succeed")
+    out = str(tmp_path / "err")
+    t0 = time.monotonic()
+    rc = spawn_ranks(2, [os.path.join(ROOT, "tests", "rank_worker_hf_error.py"), out, who])
+    assert rc == 0 and time.monotonic() - t0 < 60
+    msgs = [open(f"{out}.{r}").read() for r in range(2)]
+    assert msgs[0] == msgs[1] and match in msgs[0], msgs

@@ -21,8 +21,13 @@ def test_traffic_stamp_matches_kernel_sources(config):
         f"{bench.source_sha()}: run scripts/refresh_profiles.sh on a GPU box and "
         f"scripts/install_profiles.py")
     assert d["hbm_bytes_per_launch"] > 0
+    # ... which is also the id the built library carries (pt_build_id) and the
+    # one bench.py checks the stamp against (the loaded library's)
+    from pathtracerpython_amd import build
+    assert d["source_sha"] == build.embedded_build_id(build.OUT)
     traffic, src = bench.load_traffic(config)
     assert traffic == d["hbm_bytes_per_launch"] and src
+    assert d.get("statistic", "median") == "median"   # one statistic for every kernel
 
 
 def test_source_sha_covers_the_kernel_sources():

@@ -118,6 +118,23 @@ def test_cli_checkpoint_needs_chunks(tmp_path):
         cli.main([CORNELL, "-r", "2", "--checkpoint", str(tmp_path / "x.npz")])
 
 
+def test_cli_chunks_need_one_device(tmp_path, monkeypatch):
+    """--devices 2 with --chunk-spp (and --checkpoint) is refused
+    in the parent, before any rank process starts (it used to render in one
+    shot, ignoring both flags)."""
+    from conftest import CORNELL
+    from pathtracerpython_amd import launch
+    from pathtracerpython_amd import main as cli
+
+    def no_spawn(*a, **k):
+        raise AssertionError("rank processes started")
+    monkeypatch.setattr(launch, "spawn_ranks", no_spawn)
+    for extra in ([], ["--checkpoint", str(tmp_path / "x.npz")]):
+        with pytest.raises(SystemExit, match="--chunk-spp runs on one device"):
+            cli.main([CORNELL, "-r", "4", "--devices", "2", "--chunk-spp", "2"] + extra)
+    assert not (tmp_path / "x.npz").exists()
+
+
 def test_render_devices_validation(cornell):
     from pathtracerpython_amd.render import render
     with pytest.raises(ValueError, match="devices"):
