@@ -212,7 +212,7 @@ def injected_leg(run, rank):
     raise ValueError(f"PT_BENCH_INJECT_DEVICE_LEG={spec!r}: raise:R or hang:R")
 
 
-def bounded_leg(run, timeout_s, name, rank, world, dist, on_timeout, poll_s=0.2):
+def bounded_leg(run, timeout_s, name, rank, world, dist, on_timeout, poll_s=0.2, cleanup=None):
     """Run the secondary transport `run()` on every rank AFTER the headline
     result is complete, bounded and non-fatal: returns
     (value or None, error or None).
@@ -226,7 +226,8 @@ def bounded_leg(run, timeout_s, name, rank, world, dist, on_timeout, poll_s=0.2)
         RCCL collective that never completes): rank 0's on_timeout(message)
         prints the line with the headline and that error, and every rank ends
         with status 0 — os._exit, since a thread blocked inside a collective
-        cannot be unwound."""
+        cannot be unwound (cleanup(), e.g. removing the shared frame's file,
+        runs first)."""
     lock = threading.Lock()
     done = threading.Event()
     store = dist.distributed_c10d._get_default_store() if world > 1 else None
@@ -247,8 +248,19 @@ def bounded_leg(run, timeout_s, name, rank, world, dist, on_timeout, poll_s=0.2)
             if done.is_set():
                 return
             print(f"bench: {msg}; ending the job with the headline result", file=sys.stderr, flush=True)
+            if store is not None:   # the peers report it too
+                try:
+                    if not store.check([keys[rank]]):
+                        store.set(keys[rank], msg)
+                except Exception:   # noqa: BLE001 (the store's host is gone)
+                    pass
             if rank == 0:
                 on_timeout(msg)
+            if cleanup is not None:
+                try:
+                    cleanup()
+                except Exception:   # noqa: BLE001 (best effort on the way out)
+                    pass
             sys.stdout.flush()
             sys.stderr.flush()
             os._exit(0)
@@ -261,9 +273,13 @@ def bounded_leg(run, timeout_s, name, rank, world, dist, on_timeout, poll_s=0.2)
             except Exception:   # noqa: BLE001 (the store went away: the job is ending)
                 errs = []
             if errs:
-                fire(errs[0])
+                fire("; ".join(errs))
             if time.monotonic() > t_end:
                 fire(f"{name}: no outcome within {timeout_s:.0f} s (watchdog on rank {rank})")
+    if world > 1:
+        # the budget starts when every rank is here (rank 0 checked parity
+        # meanwhile); the control group is gloo, not the transport under test
+        dist.barrier()
     th = threading.Thread(target=monitor, daemon=True)
     th.start()
     try:
@@ -283,7 +299,8 @@ def bounded_leg(run, timeout_s, name, rank, world, dist, on_timeout, poll_s=0.2)
                 time.sleep(poll_s)
         except Exception as e:   # noqa: BLE001 (the store's host, rank 0, is gone)
             fire(f"{name}: the ranks' store is gone ({type(e).__name__}: {e})")
-        err = next((o for _, o in got if o != "ok"), None)
+        errs = [o for _, o in got if o != "ok"]   # every rank's (one may follow from another)
+        err = "; ".join(errs) if errs else None
     with lock:
         done.set()
     th.join()
@@ -400,7 +417,7 @@ def run_device_frame(ctx, steps, warmup):
 
 def main():
     args = parse()
-    from pathtracerpython_amd.launch import pg_timeout, rank_env, spawn_ranks, under_launcher
+    from pathtracerpython_amd.launch import init_gloo, pg_timeout, rank_env, spawn_ranks, under_launcher
     if args.gpus > 1 and not under_launcher():
         sys.exit(spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     import numpy as np
@@ -423,7 +440,7 @@ def main():
         # over ranks) runs over gloo on the host: the headline (host frame)
         # needs no collective on the GPUs, and a failing RCCL leg cannot take
         # it down; the device-frame leg makes its own RCCL group for its gather
-        dist.init_process_group("gloo", timeout=pg_timeout())
+        init_gloo()
 
     from oracle.oracle import host_threads
     from pathtracerpython_amd import scene_reader
@@ -631,25 +648,32 @@ def main():
         run = device_mode if other_name == "device" else (lambda: host_mode(nxt))
     budget = float(os.environ.get("PT_BENCH_LEG_TIMEOUT_S", "0")) or \
         120.0 + 4.0 * (args.steps + args.warmup) * ms_per_step * 1e-3
-    finish_line(result, other_name, run, budget, rank, world, dist, head_fb=fb)
-    if world > 1:
+    ok = finish_line(result, other_name, run, budget, rank, world, dist, head_fb=fb,
+                     cleanup=hf.discard if hf is not None else None)
+    # after a failed leg the peers may be gone: no collective in the teardown
+    if world > 1 and ok:
         dist.barrier()
     if hf is not None:
         hf.close()
     r.close()
-    if world > 1:
+    if world > 1 and ok:
         dist.barrier()
         dist.destroy_process_group()
+    if world > 1 and not ok:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     return result
 
 
-def finish_line(result, other_name, run, budget_s, rank, world, dist, head_fb=None):
+def finish_line(result, other_name, run, budget_s, rank, world, dist, head_fb=None, cleanup=None):
     """The end of a bench job, on every rank: the other frame transport
     `run()` (or a dict saying why it is skipped) bounded and non-fatal
     (bounded_leg), then rank 0 prints its line — with the other transport's
     legs, or its error — exactly once.  `result`: rank 0's complete line
     (None elsewhere); head_fb: the headline's last frame on rank 0, compared
-    bit for bit with the other transport's."""
+    bit for bit with the other transport's.  Returns False when the leg
+    failed: its peers may have left, so no collective may follow."""
     import numpy as np
     out = LineOut()
     if isinstance(run, dict):
@@ -659,7 +683,7 @@ def finish_line(result, other_name, run, budget_s, rank, world, dist, head_fb=No
             result["frame_modes"][other_name] = {"error": msg}
             out.emit(result)
         other, err = bounded_leg(injected_leg(run, rank), budget_s, f"{other_name}-frame leg", rank,
-                                 world, dist, on_timeout)
+                                 world, dist, on_timeout, cleanup=cleanup)
     if rank == 0:
         if err:
             other = {"error": err}
@@ -669,7 +693,7 @@ def finish_line(result, other_name, run, budget_s, rank, world, dist, head_fb=No
         result["frame_modes"][other_name] = {k: v for k, v in other.items() if not k.startswith("_")}
         out.emit(result)
     exit_guard(120.0)   # the line is out: a hanging teardown must not hold the job
-    return result
+    return err is None
 
 
 def k5_check_pixels(W, H):

@@ -84,5 +84,16 @@ def build(force=False, verbose=True):
     return compile_lib(OUT, verbose=verbose)
 
 
+def build_variant(name, defines):
+    """Dev: the library with compile-time switches (-D...) as
+    _lib/variants/<name>.so, for the timing scripts (PT_HIP_LIB)."""
+    return compile_lib(os.path.join(HERE, "_lib", "variants", name + ".so"), defines, verbose=False)
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    # python -m pathtracerpython_amd.build [--force]
+    # python -m pathtracerpython_amd.build --variant NAME FOO=1 BAR=2 ...
+    if len(sys.argv) > 2 and sys.argv[1] == "--variant":
+        print(build_variant(sys.argv[2], sys.argv[3:]))
+    else:
+        build(force="--force" in sys.argv)

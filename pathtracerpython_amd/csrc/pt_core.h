@@ -252,9 +252,21 @@ PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t 
 }
 
 // One Philox4x32-10 block: slots 4 blk .. 4 blk + 3 of (pixel, sample, bounce)
+#ifndef PT_RNG_KEY_OPQ
+#define PT_RNG_KEY_OPQ 0
+#endif
 PT_HD void rng_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t blk,
                      uint32_t c[4]) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#if PT_RNG_KEY_OPQ == 1 && defined(__HIP_DEVICE_COMPILE__)
+    // the round keys from the seed at each call (two scalar adds per round)
+    // instead of 20 precomputed keys held in SGPRs across the bounce loop
+    asm volatile("" : "+s"(k0), "+s"(k1));
+#elif PT_RNG_KEY_OPQ == 2 && defined(__HIP_DEVICE_COMPILE__)
+    // the same with a pure asm that takes the (loop-variant) bounce as an
+    // input: not hoistable out of the bounce loop, no side effects
+    asm("" : "+s"(k0), "+s"(k1) : "v"(bounce));
+#endif
     c[0] = pixel; c[1] = sample; c[2] = bounce; c[3] = blk;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -354,7 +366,11 @@ PT_HD RayPlane ray_plane(const UnitF& U, float h, F3 d, float hi_lo, float hi_hi
     RayPlane p;
     const float q = lin3(U.n, d);
     p.q = q;
+#if PT_ABL_RCP3   // timing ablation only: two more dependent v_rcp_f32 (the cost of one)
+    const float r = rcpf(rcpf(rcpf(q)));
+#else
     const float r = rcpf(q);
+#endif
     p.t = -h * r;
     p.at = fabsf(p.t);
     // |t_ref - t| <= (eh + |t| eq) / |q|  (eq absorbs the 3u|t| of 1/q and t)

@@ -296,6 +296,9 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double u[12], ShadowS
 #ifndef PT_RNG_PERBLOCK
 #define PT_RNG_PERBLOCK 1
 #endif
+#ifndef PT_UNIT_PREFETCH
+#define PT_UNIT_PREFETCH 0
+#endif
 // The candidate margins propagate NaN (v_minimum: a NaN compare is "not a
 // candidate" in classify_tri); the ambiguity margins drop it (fminf: a NaN
 // compare is "not certainly out").
@@ -1670,8 +1673,29 @@ PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& 
         PT_PHASE(0, c1 - c0);
         if (!FORCE64 && !COUNT && PT_MARGIN) {   // occlusion as margins (> 0: occluded)
             float oc[kLightSamples] = {-1.0f, -1.0f, -1.0f};
+#if PT_UNIT_PREFETCH
+            // the next unit's record (its first PT_UNIT_PREFETCH*16 words)
+            // loaded one unit ahead: the scalar loads overlap this unit's tests
+            UnitF Un;
+            if (S.n_obj_unit > 0) Un = S.unit[0];
+#endif
             for (int u = 0; u < S.n_obj_unit; ++u) {
+#if PT_UNIT_PREFETCH
+                UnitF U = Un;
+                {
+                    const int un = u + 1 < S.n_obj_unit ? u + 1 : u;
+                    const uint32_t* src = (const uint32_t*)&S.unit[un];
+                    uint32_t* dst = (uint32_t*)&Un;
+#pragma unroll
+                    for (int i = 0; i < 16 * PT_UNIT_PREFETCH; ++i) dst[i] = src[i];
+                    const uint32_t* cur = (const uint32_t*)&S.unit[u];
+                    uint32_t* du = (uint32_t*)&U;
+#pragma unroll
+                    for (int i = 16 * PT_UNIT_PREFETCH; i < 32; ++i) du[i] = cur[i];
+                }
+#else
                 const UnitF U = S.unit[u];
+#endif
                 const OriginU O = PT_QUAD ? origin_q(U, o32u) : origin_u(U, o32u);
                 const bool do_shadow =
                     PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));

@@ -337,6 +337,15 @@ class HostFrame:
             except FileNotFoundError:
                 pass
 
+    def discard(self):
+        """On the way out of a process that cannot close() cleanly (renders
+        may still be writing): remove the shared file (rank 0), nothing else."""
+        if self.owner:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
     def __enter__(self):
         return self
 

@@ -87,6 +87,21 @@ def spawn_ranks(n, argv, python=None, poll_s=0.05):
         _stop(procs)   # (KeyboardInterrupt, a failed Popen: no orphans)
 
 
+def init_gloo():
+    """The ranks' gloo process group (the control plane), with gloo's
+    connection messages (C++ writes to stdout) sent to stderr: rank 0's stdout
+    carries the one result line of bench.py."""
+    import torch.distributed as dist
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        dist.init_process_group("gloo", timeout=pg_timeout())
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def rank_env():
     """(rank, local_rank, world) from the environment (1 process: 0, 0, 1)."""
     return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),

@@ -18,9 +18,9 @@ def rank_main():
     import torch
     import torch.distributed as dist
     import bench
-    from pathtracerpython_amd.launch import pg_timeout, rank_env
+    from pathtracerpython_amd.launch import init_gloo, rank_env
     rank, _, world = rank_env()
-    dist.init_process_group("gloo", timeout=pg_timeout())
+    init_gloo()
     result = None
     if rank == 0:
         result = {"metric": bench.METRIC, "value": 3052.0, "unit": "Mpath-samples/s", "n_gpus": world,
@@ -36,9 +36,14 @@ def rank_main():
         dist.all_reduce(t)
         return {"ms_per_step": 5.6, "value": 3000.0, "legs_ms": {"gather": float(t[0])}}
     budget = float(os.environ.get("PT_BENCH_LEG_TIMEOUT_S", "60"))
-    bench.finish_line(result, "device", leg, budget, rank, world, dist)
-    dist.barrier()
-    dist.destroy_process_group()
+    if rank == 0:   # bench.py's rank 0 checks parity before the leg while the others wait
+        import time
+        time.sleep(float(os.environ.get("PT_TEST_RANK0_DELAY", "0")))
+    if bench.finish_line(result, "device", leg, budget, rank, world, dist):
+        dist.barrier()   # bench.main's teardown: collectives only after a clean leg
+        dist.destroy_process_group()
+    else:
+        os._exit(0)
 
 
 if __name__ == "__main__":

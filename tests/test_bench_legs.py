@@ -18,8 +18,8 @@ from conftest import ROOT
 WORKER = os.path.join(ROOT, "tests", "bench_leg_worker.py")
 
 
-def run(world, inject=None, timeout_s=None):
-    env = dict(os.environ)
+def run(world, inject=None, timeout_s=None, delay0=0):
+    env = dict(os.environ, PT_TEST_RANK0_DELAY=str(delay0))
     env.pop("PT_BENCH_INJECT_DEVICE_LEG", None)
     if inject:
         env["PT_BENCH_INJECT_DEVICE_LEG"] = inject
@@ -28,7 +28,9 @@ def run(world, inject=None, timeout_s=None):
     t0 = time.monotonic()
     res = subprocess.run([sys.executable, WORKER, "spawn", str(world)], env=env, capture_output=True,
                          text=True, timeout=240)
-    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    lines = [ln for ln in res.stdout.splitlines() if ln.strip()]
+    # rank 0's stdout is the one line (gloo's messages go to stderr)
+    assert all(ln.startswith("{") for ln in lines), res.stdout[-2000:]
     return res, [json.loads(ln) for ln in lines], time.monotonic() - t0
 
 
@@ -57,12 +59,13 @@ def test_secondary_leg_raises(who):
     assert dt < 60
 
 
-@pytest.mark.parametrize("who", [0, 1])
-def test_secondary_leg_hangs(who):
+@pytest.mark.parametrize("who,delay0", [(0, 0), (1, 0), (1, 6)])
+def test_secondary_leg_hangs(who, delay0):
     """The leg never returns on one rank (a collective that never completes):
     the watchdogs end every rank after the budget, rank 0's printing the
-    headline line with the error first."""
-    res, lines, dt = run(2, inject=f"hang:{who}", timeout_s=4)
+    headline line with the error first.  The budget counts from when every
+    rank has reached the leg (delay0: rank 0 arrives later than the budget)."""
+    res, lines, dt = run(2, inject=f"hang:{who}", timeout_s=4, delay0=delay0)
     assert res.returncode == 0, res.stderr[-2000:]
     assert len(lines) == 1
     check_headline(lines[0], 2)

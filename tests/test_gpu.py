@@ -713,12 +713,13 @@ def test_bench_headline_survives_a_failing_secondary_leg(inject):
                           "--warmup", "1", "--no-cpu-baseline"], env=env, capture_output=True, text=True,
                          timeout=240)
     assert res.returncode == 0, res.stderr[-3000:]
-    lines = [json.loads(ln) for ln in res.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1
+    lines = [ln for ln in res.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, res.stdout[-2000:]   # the one line, nothing else on stdout
+    lines = [json.loads(lines[0])]
     line = lines[0]
     assert line["n_gpus"] == 2 and line["value"] > 0 and line["config"]["frame"] == "host"
     assert line["frame_modes"]["host"]["legs_ms"]["band_kernel_max"] > 0
     assert line["linf_checked"] == "all 262144 pixels" and line["pixels_over"]["1e-6"] == 0
     err = line["frame_modes"]["device"]["error"]
     assert ("rank 1: RuntimeError: injected" in err) if inject.startswith("raise") else \
-        ("no outcome within 10 s" in err)
+        ("no outcome within 10 s" in err), err
