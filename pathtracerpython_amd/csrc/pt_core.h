@@ -253,7 +253,7 @@ PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t 
 
 // One Philox4x32-10 block: slots 4 blk .. 4 blk + 3 of (pixel, sample, bounce)
 #ifndef PT_RNG_KEY_OPQ
-#define PT_RNG_KEY_OPQ 0
+#define PT_RNG_KEY_OPQ 2
 #endif
 PT_HD void rng_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t blk,
                      uint32_t c[4]) {
@@ -332,6 +332,34 @@ PT_HD bool eval64(const TriD& T, D3 o, D3 dn, D3* P, double* sqd) {
     return dot(c1, c2) > 0.0 && dot(c1, c3) > 0.0;
 }
 
+// eval64 with the record read stage by stage (the plane, then each edge with
+// its vertex), the same operations in the same order (bit-identical): for the
+// walk kernels' rare f64 fallbacks, whose peak register demand — all 26
+// doubles of the record loaded at once — sets the walks' occupancy.
+// PT_STAGE() keeps the scheduler from hoisting a later stage's loads.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PT_STAGE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define PT_STAGE()
+#endif
+PT_HD bool eval64_lean(const TriD& T, D3 o, D3 dn, D3* P, double* sqd) {
+    const D3 vp = ld3(T.vp);
+    const double den = dot(dn, vp);
+    if (!(fabs(den) > kZero)) return false;
+    const double t = (T.cvp - dot(vp, o)) * rcp_d(dot(vp, dn));
+    const D3 p = o + dn * t;
+    *P = p;
+    *sqd = squared_dist(p, o);
+    PT_STAGE();
+    const D3 c1 = cross(ld3(T.e12), p - ld3(T.v2));
+    PT_STAGE();
+    const D3 c2 = cross(ld3(T.e23), p - ld3(T.v3));
+    if (!(dot(c1, c2) > 0.0)) return false;
+    PT_STAGE();
+    const D3 c3 = cross(ld3(T.e31), p - ld3(T.v1));
+    return dot(c1, c3) > 0.0;
+}
+
 // --------------------------------------------------------- f32 filter --
 PT_HD float aff3(const float g[3], float c, F3 x) {
     return fmaf(g[0], x.x, fmaf(g[1], x.y, fmaf(g[2], x.z, c)));
@@ -362,7 +390,10 @@ struct RayPlane {
     bool rmiss;    // |t| certainly out of range: the test is a certain miss
     bool rcand;    // |t| certainly in range and |q| certainly > 1e-5
 };
-PT_HD RayPlane ray_plane(const UnitF& U, float h, F3 d, float hi_lo, float hi_hi) {
+// eh, eo: U.eh, U.eo (the render loop passes VGPR copies made once per unit:
+// a VOP3 reads one SGPR, so two record constants in one fma cost a v_mov per
+// ray otherwise, PT_VCONST)
+PT_HD RayPlane ray_plane_e(const UnitF& U, float h, F3 d, float hi_lo, float hi_hi, float eh, float eo) {
     RayPlane p;
     const float q = lin3(U.n, d);
     p.q = q;
@@ -374,13 +405,16 @@ PT_HD RayPlane ray_plane(const UnitF& U, float h, F3 d, float hi_lo, float hi_hi
     p.t = -h * r;
     p.at = fabsf(p.t);
     // |t_ref - t| <= (eh + |t| eq) / |q|  (eq absorbs the 3u|t| of 1/q and t)
-    p.dt = fabsf(r) * fmaf(p.at, U.eq, U.eh);
+    p.dt = fabsf(r) * fmaf(p.at, U.eq, eh);
     // the unit's bound coefficients are the max over its triangles, so one
     // del serves both
-    p.del = fmaf(U.g, p.dt, fmaf(p.at, U.ed, U.eo));
+    p.del = fmaf(U.g, p.dt, fmaf(p.at, U.ed, eo));
     p.rmiss = (p.at + p.dt < kTzLo) | (p.at - p.dt >= hi_hi);
     p.rcand = (fabsf(q) > U.qhi) & (p.at - p.dt > kTzHi) & (p.at + p.dt < hi_lo);
     return p;
+}
+PT_HD RayPlane ray_plane(const UnitF& U, float h, F3 d, float hi_lo, float hi_hi) {
+    return ray_plane_e(U, h, d, hi_lo, hi_hi, U.eh, U.eo);
 }
 
 // Barycentric part (per ray and triangle), branch-free.  With

@@ -78,9 +78,11 @@ PT_HD void closest_add(ClosestAcc* c, int t, float a, float b) {
 
 // Origin terms of a unit (shared by every ray from the same origin): the
 // plane distance and each triangle's barycentric forms at the origin.
-struct OriginU { float h, bo0, co0, bo1, co1; };
+struct OriginU { float h, bo0, co0, bo1, co1, eh = 0.f, eo = 0.f; };
 PT_HD OriginU origin_u(const UnitF& U, F3 o) {
     OriginU r;
+    r.eh = U.eh;
+    r.eo = U.eo;
     r.h = aff3(U.n, U.cn, o);
     r.bo0 = aff3(U.tri[0].gb, U.tri[0].cb, o);
     r.co0 = aff3(U.tri[0].gc, U.tri[0].cc, o);
@@ -358,9 +360,18 @@ PT_HD QuadM quad_m(const UnitF& U, const RayPlane& p, const OriginU& O, F3 d) {
     return r;
 }
 // origin terms of the render loop's unit form (the second member's only for
-// a pair that is no parallelogram)
+// a pair that is no parallelogram), and (PT_VCONST) VGPR copies of the
+// record's eh and eo for ray_plane_e
+#ifndef PT_VCONST
+#define PT_VCONST 1
+#endif
 PT_HD OriginU origin_q(const UnitF& U, F3 o) {
     OriginU r;
+    r.eh = U.eh;
+    r.eo = U.eo;
+#if PT_VCONST && defined(__HIP_DEVICE_COMPILE__)
+    asm("" : "+v"(r.eh), "+v"(r.eo));   // (pure: once per unit, no side effects)
+#endif
     r.h = aff3(U.n, U.cn, o);
     r.bo0 = aff3(U.tri[0].gb, U.tri[0].cb, o);
     r.co0 = aff3(U.tri[0].gc, U.tri[0].cc, o);
@@ -371,13 +382,20 @@ PT_HD OriginU origin_q(const UnitF& U, F3 o) {
     }
     return r;
 }
+// PT_AMB_MAX: the shadow rays' ambiguity is kept as one running maximum per
+// lane and unit (amax >= 0: some test needs f64) instead of per-test bits —
+// one v_max3 per ray instead of six bit-packing instructions; the rare block
+// rebuilds the bits (shadow_bits_m)
+#ifndef PT_AMB_MAX
+#define PT_AMB_MAX 1
+#endif
 PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
-                         ShadowSet* sh, float oc[kLightSamples], uint32_t* amb) {
+                         ShadowSet* sh, float oc[kLightSamples], uint32_t* amb, float* amax = nullptr) {
     const float cop = coplanar ? -1.0f : INFINITY;
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
         const F3 d = sh->d32[k];
-        const RayPlane p = ray_plane(U, O.h, d, sh->hlo[k], sh->hhi[k]);
+        const RayPlane p = ray_plane_e(U, O.h, d, sh->hlo[k], sh->hhi[k], O.eh, O.eo);
         float cm, nm;
         margin_plane(U, p, sh->hlo[k], sh->hhi[k], cop, &cm, &nm);
         // nm < 0 (the plane part is a certain miss; nm is never NaN, cop is
@@ -405,12 +423,44 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
                 sh->key2 = U.obj;
                 sh->leak = U.obj;
             }
-            if (need) *amb |= (a0 >= 0.0f ? 1u : 0u) << (2 * k) | (a1 >= 0.0f ? 2u : 0u) << (2 * k);
+            if (PT_AMB_MAX && amax) *amax = fmaxf(*amax, need ? fmaxf(a0, a1) : -1.0f);
+            else if (need) *amb |= (a0 >= 0.0f ? 1u : 0u) << (2 * k) | (a1 >= 0.0f ? 2u : 0u) << (2 * k);
+        } else if (PT_AMB_MAX && amax) {   // only while not occluded before this unit
+            *amax = fmaxf(*amax, fmaxf(fminf(a0, -old), fminf(a1, -old)));
         } else {   // only while not occluded before this unit
             *amb |= (fminf(a0, -old) >= 0.0f ? 1u : 0u) << (2 * k) |
                     (fminf(a1, -old) >= 0.0f ? 2u : 0u) << (2 * k);
         }
     }
+}
+// The shadow bits of shadow_unit_m rebuilt after the unit (PT_AMB_MAX, the
+// rare path; no vote).  oc and key2 are already updated by this unit: a ray it
+// occluded for certain gets no bits here where shadow_unit_m set some, and the
+// f64 block would skip those ("decided meanwhile"), so the decisions are the
+// same.
+PT_HD uint32_t shadow_bits_m(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
+                             const ShadowSet* sh, const float oc[kLightSamples]) {
+    const float cop = coplanar ? -1.0f : INFINITY;
+    uint32_t amb = 0;
+#pragma unroll
+    for (int k = 0; k < kLightSamples; ++k) {
+        const F3 d = sh->d32[k];
+        const RayPlane p = ray_plane(U, O.h, d, sh->hlo[k], sh->hhi[k]);
+        float cm, nm;
+        margin_plane(U, p, sh->hlo[k], sh->hhi[k], cop, &cm, &nm);
+        if (nm < 0.0f) continue;   // every margin negative: no ambiguous test
+        const QuadM m = quad_m(U, p, O, d);
+        float c0, a0, c1, a1;
+        margin_m(m.m0, p, cm, nm, &c0, &a0);
+        margin_m(m.m1, p, cm, nm, &c1, &a1);
+        if (k == kLightSamples - 1) {
+            if (U.obj < sh->key2) amb |= (a0 >= 0.0f ? 1u : 0u) << (2 * k) | (a1 >= 0.0f ? 2u : 0u) << (2 * k);
+        } else {
+            amb |= (fminf(a0, -oc[k]) >= 0.0f ? 1u : 0u) << (2 * k) |
+                   (fminf(a1, -oc[k]) >= 0.0f ? 2u : 0u) << (2 * k);
+        }
+    }
+    return amb;
 }
 
 // The f64 decisions of a unit's ambiguous tests (bits of amb, see
@@ -484,8 +534,9 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
     // lines that reached the leaf's box; a line that did not cannot hit)
     uint32_t amb = 0;   // bit 2k+i: shadow ray k / triangle i; bit 6+i: closest / triangle i
     const bool two = (U.count == 2);
+    float amax = -1.0f;   // PT_AMB_MAX: >= 0 when some shadow test of the unit is ambiguous
     if (MARGIN) {   // the render loop's uniform units (oc: occlusion margins)
-        if (do_shadow) shadow_unit_m(S, U, O, coplanar, sh, oc, &amb);
+        if (do_shadow) shadow_unit_m(S, U, O, coplanar, sh, oc, &amb, PT_QUAD ? &amax : nullptr);
     } else if (do_shadow) {   // (sh is only touched here and for shadow bits: null without shadows)
         bool occ0[kLightSamples];
 #pragma unroll
@@ -525,7 +576,8 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
         }
     }
     if (!FORCE64 && do_closest && (rays & 8u)) {
-        const RayPlane p = ray_plane(U, O.h, n32, INFINITY, INFINITY);
+        const RayPlane p = (MARGIN && PT_QUAD) ? ray_plane_e(U, O.h, n32, INFINITY, INFINITY, O.eh, O.eo)
+                                               : ray_plane(U, O.h, n32, INFINITY, INFINITY);
         bool c0, a0, c1 = false, a1 = false;
         if (MARGIN && PT_QUAD) {   // the render loop's unit form (quad_m)
             const QuadM m = quad_m(U, p, O, n32);
@@ -551,7 +603,12 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
                     c ? p.at + p.dt : INFINITY);
         amb |= (a0 ? 64u : 0u) | (a1 ? 128u : 0u);
     }
+    if (PT_AMB_MAX && MARGIN && PT_QUAD && (PARTS & 1) && !(amax < 0.0f))   // rare: rebuild the bits
+        amb |= shadow_bits_m(S, U, O, coplanar, sh, oc);
     amb &= ((PARTS & 1) ? 0x3fu : 0u) | ((PARTS & 2) ? 0xc0u : 0u);
+#if PT_ABL_WALK_NOFB   // timing ablation only (wrong output): no f64 fallback in the closest walks
+    if (PARTS == 2) amb = 0;
+#endif
     if (amb) fused_fallback<FORCE64, COUNT, MARGIN, PARTS>(S, U, amb, sh, ca, sp, cnt, oc);   // rare (FORCE64: every shadow test) — decide in f64
 }
 
@@ -1302,6 +1359,14 @@ struct Shadow1 {
 PT_HD bool shadow1_open(const SceneK& S, const Shadow1& r) {
     return r.k == kLightSamples - 1 ? r.key2 > S.bvh_min_obj : !r.occ;
 }
+#ifndef PT_WALK_LEAN
+#define PT_WALK_LEAN 0
+#endif
+#if PT_WALK_LEAN
+#define PT_WALK_EVAL64 eval64_lean
+#else
+#define PT_WALK_EVAL64 eval64
+#endif
 // the f64 decisions of a unit's ambiguous tests for the ray (a0, a1)
 // (inline: an out-of-line call's frame made the walk 2x slower)
 PT_HD void shadow1_fallback(const SceneK& S, const UnitF& U, bool a0, bool a1, Shadow1* r,
@@ -1314,7 +1379,7 @@ PT_HD void shadow1_fallback(const SceneK& S, const UnitF& U, bool a0, bool a1, S
         if (last ? (U.obj >= r->key2) : r->occ) continue;   // decided meanwhile
         D3 Q;
         double sqd;
-        if (eval64(S.trid[U.t[i]], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
+        if (PT_WALK_EVAL64(S.trid[U.t[i]], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
             sqd < squared_dist(P, L)) {
             r->occ = true;
             if (last) {
@@ -1349,7 +1414,11 @@ PT_HD void shadow1_unit(const SceneK& S, const UnitF& U, F3 o32, int ogrp, Shado
             r->leak = U.obj;
         }
     }
+#if PT_ABL_WALK_NOFB   // timing ablation only (wrong output): no f64 fallback in the walk
+    (void)need;
+#else
     if (need && (a0 | a1)) shadow1_fallback(S, U, a0, a1, r, sp);
+#endif
 }
 struct ShadowTrav1 {
     F3 o32, inv;

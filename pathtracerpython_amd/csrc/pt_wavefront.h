@@ -30,7 +30,9 @@
 
 namespace pt {
 
-enum : int32_t { kWfDone = 0, kWfPrimary = 1, kWfBounce = 2 };
+// kWfBegin: the slot's pending work is finished and its next bounce is to be
+// started (the split shade step: wf_finish, then wf_begin_bounce)
+enum : int32_t { kWfDone = 0, kWfPrimary = 1, kWfBounce = 2, kWfBegin = 3 };
 
 // Two 128-B lines per slot: the first holds everything a shade step reads
 // and writes (the per-step fields and the spill slots P, Nd), the second the
@@ -260,12 +262,13 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
     return want;
 }
 
-// Shade step >= 1: finish the pending work of the slot with the walks'
-// results, then start its next bounce.  Returns the queries wanted.
-// pq: the slot's primary query (the GPU shares one per pixel, k_wf_primary;
-// the host emulation has one per slot, cq)
-PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfShadowQ* shq,
-                        WfClosestQ* cq, const WfClosestQ* pq) {
+// Shade step >= 1, first half: finish the pending work of the slot with the
+// walks' results (the colour, the next hit, path end / next sample).  Returns
+// true when the slot's next bounce is to be started (state kWfBegin; the
+// second half is wf_begin_bounce).  pq: the slot's primary query (the GPU
+// shares one per pixel, k_wf_primary; the host emulation has one per slot, cq)
+PT_HD bool wf_finish(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, const WfShadowQ* shq,
+                     const WfClosestQ* cq, const WfClosestQ* pq) {
     const Spill sp{W->sp, 1};
     if (W->state() == kWfPrimary) {   // k_render: closest(eye, d0) then render_lane's prologue
         D3 P0 = d3(0, 0, 0);
@@ -277,10 +280,10 @@ PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfS
             for (int i = 0; i < J.n_samples; ++i) acc = acc + v;
             W->acc[0] = acc.x; W->acc[1] = acc.y; W->acc[2] = acc.z;
             W->set(kWfDone, false, 0);
-            return 0;
+            return false;
         }
         W->si = 0;
-        W->set(kWfPrimary, false, 0);   // (b = 0; begin_bounce sets the state)
+        W->set(kWfBegin, false, 0);   // (b = 0; begin_bounce sets the state)
         W->tri = tri0;
         W->tri0 = tri0;
         W->k = 1.0;
@@ -289,9 +292,9 @@ PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfS
         sp.put3(kSpP0, P0);
         sp.put3(kSpP, P0);
         sp.put3(kSpNd, d0);   // incoming direction of bounce 0 (main.py:191)
-        return wf_begin_bounce(S, J, W, shq, cq);
+        return true;
     }
-    if (W->state() != kWfBounce) return 0;
+    if (W->state() != kWfBounce) return false;
     // the colour of the pending bounce (main.py:208-231)
     ShadowSet sh;
 #pragma unroll
@@ -339,10 +342,26 @@ PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfS
     W->si = si;
     if (si >= J.n_samples) {
         W->set(kWfDone, false, 0);
-        return 0;
+        return false;
     }
-    W->set(kWfBounce, false, b);   // (begin_bounce sets trace)
-    return wf_begin_bounce(S, J, W, shq, cq);
+    W->set(kWfBegin, false, b);   // (begin_bounce sets the state and trace)
+    return true;
+}
+
+// Shade step >= 1: wf_finish, then the next bounce's start.  Returns the
+// queries wanted.  (The GPU runs the two halves as one kernel, k_wf_shade,
+// or as two, k_wf_finish + k_wf_begin: PT_WF_SPLIT.)
+#ifndef PT_WF_SHADE_TWOCALLS
+#define PT_WF_SHADE_TWOCALLS 0
+#endif
+PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfShadowQ* shq,
+                        WfClosestQ* cq, const WfClosestQ* pq) {
+#if PT_WF_SHADE_TWOCALLS   // (round 4's form: the next bounce started from two call sites)
+    if (W->state() == kWfPrimary)
+        return wf_finish(S, J, d0, W, shq, cq, pq) ? wf_begin_bounce(S, J, W, shq, cq) : 0u;
+    if (W->state() != kWfBounce) return 0u;
+#endif
+    return wf_finish(S, J, d0, W, shq, cq, pq) ? wf_begin_bounce(S, J, W, shq, cq) : 0u;
 }
 
 }  // namespace pt

@@ -5,7 +5,7 @@
 set -uo pipefail
 R=$PWD; TAG=${1:-var}
 bash "$R/scripts/pmc_k2.sh" "${TAG}_main" > /dev/null 2>&1 || exit 1
-for v in "$R"/pathtracerpython_amd/_lib/variants/*.so; do
+for v in "$R"/pathtracerpython_amd/_lib/variants/${PREFIX:-k2_}*.so; do
     [ -e "$v" ] || continue
     b=$(basename "$v" .so)
     cd "$R" && bash "$R/scripts/pmc_k2.sh" "${TAG}_$b" "$v" > /dev/null 2>&1 || exit 1

@@ -30,6 +30,9 @@ pmc() {   # pmc NAME "COUNTERS" driver args...
     timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $ctr --output-format csv \
         -d "$OUT/$name" -o p -- python3 "$@" > "$OUT/$name.log" 2>&1
 }
+# PARTS: "k2 k5" (default), or one of them (two gpurun calls)
+PARTS=${PARTS:-k2 k5}
+if [[ " $PARTS " == *" k2 "* ]]; then
 # 1-2. K2 counters (3 launches each)
 pmc k2_fetch FETCH_SIZE "$R/scripts/prof_k2.py" 3
 pmc k2_write WRITE_SIZE "$R/scripts/prof_k2.py" 3
@@ -52,6 +55,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 cp "$OUT/trace_k2/k2_kernel_stats.csv" "$P/${TAG}_k2_kernel_stats.csv"
 timeout -k 10 400 python3 "$R/bench.py" > "$P/${TAG}_bench_k2.json" 2> "$OUT/bench_k2.err"
 cat "$P/${TAG}_bench_k2.json"
+fi
+if [[ " $PARTS " == *" k5 "* ]]; then
+cd "$R"
 # 5. K5
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_k5" -o k5 \
     -- python3 "$R/bench.py" --config k5 --steps 1 --warmup 0 --no-cpu-baseline --no-check \
@@ -76,3 +82,4 @@ cd "$R"
 cp "$P/traffic_k5.json" "$R/profiles/traffic_k5.json"
 timeout -k 10 400 python3 "$R/bench.py" --config k5 > "$P/${TAG}_bench_k5.json" 2> "$OUT/bench_k5.err"
 cat "$P/${TAG}_bench_k5.json"
+fi
