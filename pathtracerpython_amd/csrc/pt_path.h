@@ -359,6 +359,9 @@ PT_HD QuadM quad_m(const UnitF& U, const RayPlane& p, const OriginU& O, F3 d) {
     }
     return r;
 }
+#ifndef PT_MICRO
+#define PT_MICRO 2
+#endif
 // origin terms of the render loop's unit form (the second member's only for
 // a pair that is no parallelogram), and (PT_VCONST) VGPR copies of the
 // record's eh and eo for ray_plane_e
@@ -377,8 +380,17 @@ PT_HD OriginU origin_q(const UnitF& U, F3 o) {
     r.co0 = aff3(U.tri[0].gc, U.tri[0].cc, o);
     r.bo1 = r.co1 = 0.f;
     if (U.quad < 0) {   // wave-uniform
+#if PT_MICRO >= 2 && defined(__HIP_DEVICE_COMPILE__)
+        // (3) an opaque copy of the origin: the compiler otherwise computes
+        // these two forms for every unit (speculated out of the branch)
+        F3 oo = o;
+        asm("" : "+v"(oo.x), "+v"(oo.y), "+v"(oo.z));
+        r.bo1 = aff3(U.tri[1].gb, U.tri[1].cb, oo);
+        r.co1 = aff3(U.tri[1].gc, U.tri[1].cc, oo);
+#else
         r.bo1 = aff3(U.tri[1].gb, U.tri[1].cb, o);
         r.co1 = aff3(U.tri[1].gc, U.tri[1].cc, o);
+#endif
     }
     return r;
 }
@@ -389,9 +401,20 @@ PT_HD OriginU origin_q(const UnitF& U, F3 o) {
 #ifndef PT_AMB_MAX
 #define PT_AMB_MAX 1
 #endif
+// PT_MICRO: (1) cop canonicalised once per unit, so the margins built from
+// it need no per-ray canonicalisation before fminf (IEEE mode), (2) the
+// ambiguity maximum taken before the occlusion margin is overwritten (no
+// register copy of the loop-carried margin), (3) origin_q above.  Same values.
+PT_HD float pt_canon(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_canonicalizef(x);
+#else
+    return x;
+#endif
+}
 PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
                          ShadowSet* sh, float oc[kLightSamples], uint32_t* amb, float* amax = nullptr) {
-    const float cop = coplanar ? -1.0f : INFINITY;
+    const float cop = PT_MICRO ? pt_canon(coplanar ? -1.0f : INFINITY) : (coplanar ? -1.0f : INFINITY);
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
         const F3 d = sh->d32[k];
@@ -416,7 +439,7 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
 #endif
         const float old = oc[k];
         const float c = fmaxf(c0, c1);
-        oc[k] = fmaxf(old, c);
+        if (!PT_MICRO) oc[k] = fmaxf(old, c);
         if (k == kLightSamples - 1) {
             const bool need = U.obj < sh->key2;
             if (c > 0.0f && need) {
@@ -431,6 +454,7 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
             *amb |= (fminf(a0, -old) >= 0.0f ? 1u : 0u) << (2 * k) |
                     (fminf(a1, -old) >= 0.0f ? 2u : 0u) << (2 * k);
         }
+        if (PT_MICRO) oc[k] = fmaxf(old, c);
     }
 }
 // The shadow bits of shadow_unit_m rebuilt after the unit (PT_AMB_MAX, the
