@@ -253,18 +253,18 @@ PT_HD void rng_blocks4(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t 
 
 // One Philox4x32-10 block: slots 4 blk .. 4 blk + 3 of (pixel, sample, bounce)
 #ifndef PT_RNG_KEY_OPQ
-#define PT_RNG_KEY_OPQ 2
+#define PT_RNG_KEY_OPQ 1
 #endif
 PT_HD void rng_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t bounce, uint32_t blk,
                      uint32_t c[4]) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#if PT_RNG_KEY_OPQ == 1 && defined(__HIP_DEVICE_COMPILE__)
-    // the round keys from the seed at each call (two scalar adds per round)
-    // instead of 20 precomputed keys held in SGPRs across the bounce loop
-    asm volatile("" : "+s"(k0), "+s"(k1));
-#elif PT_RNG_KEY_OPQ == 2 && defined(__HIP_DEVICE_COMPILE__)
-    // the same with a pure asm that takes the (loop-variant) bounce as an
-    // input: not hoistable out of the bounce loop, no side effects
+#if PT_RNG_KEY_OPQ && defined(__HIP_DEVICE_COMPILE__)
+    // The round keys from the seed at each call (two scalar adds per round)
+    // instead of 20 keys the compiler precomputes and holds in SGPRs across
+    // the bounce loop (K2: SGPR spills 65 -> 43, no scratch): an
+    // empty pure asm with the loop-variant bounce index as an input cannot
+    // be hoisted out of the loop.  (A volatile asm would count as a memory
+    // side effect and turn the unit records' scalar loads into vector loads.)
     asm("" : "+s"(k0), "+s"(k1) : "v"(bounce));
 #endif
     c[0] = pixel; c[1] = sample; c[2] = bounce; c[3] = blk;
@@ -332,34 +332,6 @@ PT_HD bool eval64(const TriD& T, D3 o, D3 dn, D3* P, double* sqd) {
     return dot(c1, c2) > 0.0 && dot(c1, c3) > 0.0;
 }
 
-// eval64 with the record read stage by stage (the plane, then each edge with
-// its vertex), the same operations in the same order (bit-identical): for the
-// walk kernels' rare f64 fallbacks, whose peak register demand — all 26
-// doubles of the record loaded at once — sets the walks' occupancy.
-// PT_STAGE() keeps the scheduler from hoisting a later stage's loads.
-#if defined(__HIP_DEVICE_COMPILE__)
-#define PT_STAGE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define PT_STAGE()
-#endif
-PT_HD bool eval64_lean(const TriD& T, D3 o, D3 dn, D3* P, double* sqd) {
-    const D3 vp = ld3(T.vp);
-    const double den = dot(dn, vp);
-    if (!(fabs(den) > kZero)) return false;
-    const double t = (T.cvp - dot(vp, o)) * rcp_d(dot(vp, dn));
-    const D3 p = o + dn * t;
-    *P = p;
-    *sqd = squared_dist(p, o);
-    PT_STAGE();
-    const D3 c1 = cross(ld3(T.e12), p - ld3(T.v2));
-    PT_STAGE();
-    const D3 c2 = cross(ld3(T.e23), p - ld3(T.v3));
-    if (!(dot(c1, c2) > 0.0)) return false;
-    PT_STAGE();
-    const D3 c3 = cross(ld3(T.e31), p - ld3(T.v1));
-    return dot(c1, c3) > 0.0;
-}
-
 // --------------------------------------------------------- f32 filter --
 PT_HD float aff3(const float g[3], float c, F3 x) {
     return fmaf(g[0], x.x, fmaf(g[1], x.y, fmaf(g[2], x.z, c)));
@@ -397,11 +369,7 @@ PT_HD RayPlane ray_plane_e(const UnitF& U, float h, F3 d, float hi_lo, float hi_
     RayPlane p;
     const float q = lin3(U.n, d);
     p.q = q;
-#if PT_ABL_RCP3   // timing ablation only: two more dependent v_rcp_f32 (the cost of one)
-    const float r = rcpf(rcpf(rcpf(q)));
-#else
     const float r = rcpf(q);
-#endif
     p.t = -h * r;
     p.at = fabsf(p.t);
     // |t_ref - t| <= (eh + |t| eq) / |q|  (eq absorbs the 3u|t| of 1/q and t)

@@ -426,45 +426,6 @@ __global__ __launch_bounds__(kShadeBlock) void k_wf_shade(SceneK S, RenderK R, i
 #endif
 }
 
-// The shade step as two launches (PT_WF_SPLIT): k_wf_finish finishes every
-// running slot's pending bounce (the walks' results, the colour, the next
-// hit, path end / next sample: a chain of dependent loads, few registers),
-// k_wf_begin starts the next bounce of the slots that need one (RNG, light
-// samples, next ray, the uniform units' pass: arithmetic) and appends the
-// queries.  Each half runs at its own occupancy; the path record's first
-// line is read by both.  The same per-slot operations as k_wf_shade
-// (wf_shade = wf_finish + wf_begin_bounce), so the same frame bit for bit.
-#ifndef PT_WF_SPLIT
-#define PT_WF_SPLIT 0
-#endif
-__global__ __launch_bounds__(256) void k_wf_finish(SceneK S, RenderK R, WfPath* __restrict__ W,
-                                                   const WfShadowQ* __restrict__ SQ,
-                                                   const WfClosestQ* __restrict__ CQ,
-                                                   const WfClosestQ* __restrict__ CQP, uint32_t slots) {
-    const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
-    if (tid < slots && (tid >> R.split_log2) < R.npix && W[tid].state() != kWfDone) {
-        const SlotJob j = slot_job(S, R, tid);
-        (void)wf_finish(S, j.J, j.d0, &W[tid], &SQ[tid], &CQ[tid], &CQP[tid >> R.split_log2]);
-    }
-}
-__global__ __launch_bounds__(kShadeBlock) void k_wf_begin(SceneK S, RenderK R, WfPath* __restrict__ W,
-                                                  WfShadowQ* __restrict__ SQ, WfClosestQ* __restrict__ CQ,
-                                                  int32_t* __restrict__ lists, int32_t* counters,
-                                                  uint32_t slots) {
-    const uint32_t tid = blockIdx.x * (uint32_t)kShadeBlock + threadIdx.x;
-    uint32_t want = 0;
-    if (tid < slots && (tid >> R.split_log2) < R.npix && W[tid].state() == kWfBegin) {
-        const SlotJob j = slot_job(S, R, tid);
-        want = wf_begin_bounce(S, j.J, &W[tid], &SQ[tid], &CQ[tid]);
-    }
-#if PT_WF_BLOCK_APPEND
-    wf_append_block(want, counters, lists, lists + 3 * (size_t)slots, (int32_t)tid);
-#else
-    wf_append3(want, &counters[0], lists, (int32_t)tid);
-    wf_append((want & kWfWantClosest) != 0, &counters[2], lists + 3 * (size_t)slots, (int32_t)tid);
-#endif
-}
-
 // Persistent walk kernels over the 4-wide quantised BVH (QNode): a
 // work-item holds one query at a time and takes the next one from the list
 // as soon as its walk ends.  A loop turn is one
@@ -1168,18 +1129,9 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     for (int32_t step = 0; step < steps; ++step) {
         HIPCHK(hipMemsetAsync(counters, 0, 4 * sizeof(int32_t), st));
         HIPCHK(mark(step, 0, 0, st));
-        if (PT_WF_SPLIT && step > 0) {
-            hipLaunchKernelGGL(k_wf_finish, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, s->dev, R,
-                               W, (const WfShadowQ*)SQ, (const WfClosestQ*)CQ, (const WfClosestQ*)CQP,
-                               (uint32_t)slots);
-            hipLaunchKernelGGL(k_wf_begin, dim3((unsigned)((slots + kShadeBlock - 1) / kShadeBlock)),
-                               dim3(kShadeBlock), 0, st, s->dev, R, W, SQ, CQ, lists, counters,
-                               (uint32_t)slots);
-        } else {
-            hipLaunchKernelGGL(k_wf_shade, dim3((unsigned)((slots + kShadeBlock - 1) / kShadeBlock)),
-                               dim3(kShadeBlock), 0, st, s->dev, R, step, W, SQ, CQ,
-                               (const WfClosestQ*)CQP, lists, counters, (uint32_t)slots);
-        }
+        hipLaunchKernelGGL(k_wf_shade, dim3((unsigned)((slots + kShadeBlock - 1) / kShadeBlock)),
+                           dim3(kShadeBlock), 0, st, s->dev, R, step, W, SQ, CQ,
+                           (const WfClosestQ*)CQP, lists, counters, (uint32_t)slots);
         if (step == 0)
             hipLaunchKernelGGL(k_wf_primary, dim3((R.npix + 255) / 256), dim3(256), 0, st, s->dev, R, W,
                                CQP, lists + 3 * slots, counters + 2);

@@ -298,9 +298,6 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double u[12], ShadowS
 #ifndef PT_RNG_PERBLOCK
 #define PT_RNG_PERBLOCK 1
 #endif
-#ifndef PT_UNIT_PREFETCH
-#define PT_UNIT_PREFETCH 0
-#endif
 // The candidate margins propagate NaN (v_minimum: a NaN compare is "not a
 // candidate" in classify_tri); the ambiguity margins drop it (fminf: a NaN
 // compare is "not certainly out").
@@ -630,9 +627,6 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
     if (PT_AMB_MAX && MARGIN && PT_QUAD && (PARTS & 1) && !(amax < 0.0f))   // rare: rebuild the bits
         amb |= shadow_bits_m(S, U, O, coplanar, sh, oc);
     amb &= ((PARTS & 1) ? 0x3fu : 0u) | ((PARTS & 2) ? 0xc0u : 0u);
-#if PT_ABL_WALK_NOFB   // timing ablation only (wrong output): no f64 fallback in the closest walks
-    if (PARTS == 2) amb = 0;
-#endif
     if (amb) fused_fallback<FORCE64, COUNT, MARGIN, PARTS>(S, U, amb, sh, ca, sp, cnt, oc);   // rare (FORCE64: every shadow test) — decide in f64
 }
 
@@ -1383,14 +1377,6 @@ struct Shadow1 {
 PT_HD bool shadow1_open(const SceneK& S, const Shadow1& r) {
     return r.k == kLightSamples - 1 ? r.key2 > S.bvh_min_obj : !r.occ;
 }
-#ifndef PT_WALK_LEAN
-#define PT_WALK_LEAN 0
-#endif
-#if PT_WALK_LEAN
-#define PT_WALK_EVAL64 eval64_lean
-#else
-#define PT_WALK_EVAL64 eval64
-#endif
 // the f64 decisions of a unit's ambiguous tests for the ray (a0, a1)
 // (inline: an out-of-line call's frame made the walk 2x slower)
 PT_HD void shadow1_fallback(const SceneK& S, const UnitF& U, bool a0, bool a1, Shadow1* r,
@@ -1403,7 +1389,7 @@ PT_HD void shadow1_fallback(const SceneK& S, const UnitF& U, bool a0, bool a1, S
         if (last ? (U.obj >= r->key2) : r->occ) continue;   // decided meanwhile
         D3 Q;
         double sqd;
-        if (PT_WALK_EVAL64(S.trid[U.t[i]], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
+        if (eval64(S.trid[U.t[i]], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
             sqd < squared_dist(P, L)) {
             r->occ = true;
             if (last) {
@@ -1438,11 +1424,7 @@ PT_HD void shadow1_unit(const SceneK& S, const UnitF& U, F3 o32, int ogrp, Shado
             r->leak = U.obj;
         }
     }
-#if PT_ABL_WALK_NOFB   // timing ablation only (wrong output): no f64 fallback in the walk
-    (void)need;
-#else
     if (need && (a0 | a1)) shadow1_fallback(S, U, a0, a1, r, sp);
-#endif
 }
 struct ShadowTrav1 {
     F3 o32, inv;
@@ -1766,29 +1748,8 @@ PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& 
         PT_PHASE(0, c1 - c0);
         if (!FORCE64 && !COUNT && PT_MARGIN) {   // occlusion as margins (> 0: occluded)
             float oc[kLightSamples] = {-1.0f, -1.0f, -1.0f};
-#if PT_UNIT_PREFETCH
-            // the next unit's record (its first PT_UNIT_PREFETCH*16 words)
-            // loaded one unit ahead: the scalar loads overlap this unit's tests
-            UnitF Un;
-            if (S.n_obj_unit > 0) Un = S.unit[0];
-#endif
             for (int u = 0; u < S.n_obj_unit; ++u) {
-#if PT_UNIT_PREFETCH
-                UnitF U = Un;
-                {
-                    const int un = u + 1 < S.n_obj_unit ? u + 1 : u;
-                    const uint32_t* src = (const uint32_t*)&S.unit[un];
-                    uint32_t* dst = (uint32_t*)&Un;
-#pragma unroll
-                    for (int i = 0; i < 16 * PT_UNIT_PREFETCH; ++i) dst[i] = src[i];
-                    const uint32_t* cur = (const uint32_t*)&S.unit[u];
-                    uint32_t* du = (uint32_t*)&U;
-#pragma unroll
-                    for (int i = 16 * PT_UNIT_PREFETCH; i < 32; ++i) du[i] = cur[i];
-                }
-#else
                 const UnitF U = S.unit[u];
-#endif
                 const OriginU O = PT_QUAD ? origin_q(U, o32u) : origin_u(U, o32u);
                 const bool do_shadow =
                     PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));

@@ -349,18 +349,11 @@ PT_HD bool wf_finish(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, const 
 }
 
 // Shade step >= 1: wf_finish, then the next bounce's start.  Returns the
-// queries wanted.  (The GPU runs the two halves as one kernel, k_wf_shade,
-// or as two, k_wf_finish + k_wf_begin: PT_WF_SPLIT.)
-#ifndef PT_WF_SHADE_TWOCALLS
-#define PT_WF_SHADE_TWOCALLS 0
-#endif
+// queries wanted.  (One call site of wf_begin_bounce: round 4 started the
+// next bounce from two, inlined twice — 141 instead of 113 VGPRs for
+// k_wf_shade, the same time)
 PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfShadowQ* shq,
                         WfClosestQ* cq, const WfClosestQ* pq) {
-#if PT_WF_SHADE_TWOCALLS   // (round 4's form: the next bounce started from two call sites)
-    if (W->state() == kWfPrimary)
-        return wf_finish(S, J, d0, W, shq, cq, pq) ? wf_begin_bounce(S, J, W, shq, cq) : 0u;
-    if (W->state() != kWfBounce) return 0u;
-#endif
     return wf_finish(S, J, d0, W, shq, cq, pq) ? wf_begin_bounce(S, J, W, shq, cq) : 0u;
 }
 
