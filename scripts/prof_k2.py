@@ -7,11 +7,12 @@ import torch
 from pathtracerpython_amd import scene_reader
 from pathtracerpython_amd.render import Renderer
 scene_reader.VERBOSE = False
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 3
 f64 = "--f64" in sys.argv
 torch.cuda.set_device(0)
 r = Renderer(scene_reader.Scene(os.path.join(ROOT, "scenes/cornell/cornellroom.sdl")))
-p = r.params(512, 512, 64, 4, 9, force_f64=f64)
+lanes = int(sys.argv[sys.argv.index("--lanes") + 1]) if "--lanes" in sys.argv else 0
+p = r.params(512, 512, 64, 4, 9, force_f64=f64, lanes_per_pixel=lanes)
 tile = torch.zeros((512, 512, 3), dtype=torch.float32, device="cuda")
 s = torch.cuda.current_stream()
 ms = []

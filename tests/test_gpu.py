@@ -723,3 +723,17 @@ def test_bench_headline_survives_a_failing_secondary_leg(inject):
     err = line["frame_modes"]["device"]["error"]
     assert ("rank 1: RuntimeError: injected" in err) if inject.startswith("raise") else \
         ("no outcome within 10 s" in err), err
+
+
+def test_rccl_gather_on_the_device(cornell, tmp_path):
+    """The device-frame transport's RCCL gather, run on the hardware as
+    bench.py runs it (gloo control plane + an nccl group for the gather,
+    tests/rank_worker_rccl.py).  A one-GPU box allows world 1 only; the
+    assembled frame equals a direct render bit for bit."""
+    from conftest import ROOT
+    from pathtracerpython_amd.launch import spawn_ranks
+    out = str(tmp_path / "frame.npy")
+    assert spawn_ranks(1, [os.path.join(ROOT, "tests", "rank_worker_rccl.py"), out]) == 0
+    with Renderer(cornell) as r:
+        ref = r.render(64, 64, 4, 3, 9)
+    assert np.array_equal(np.load(out), ref)
