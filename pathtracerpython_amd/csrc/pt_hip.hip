@@ -181,6 +181,15 @@ __device__ __forceinline__ int primary_shared(const SceneK& S, D3 eye, D3 d0, ui
 #define PT_PRIMARY_SHARED 16
 #endif
 
+// Work-items per k_render block: one wave.  Nothing in the kernel is shared
+// beyond a wave (a pixel's lanes reduce with shuffles), and the spill home
+// is LDS allocated per block: with 4-wave blocks a wave's slot stayed idle
+// until the block's slowest wave ended (its 40 KB held), with 1-wave blocks
+// it is refilled as soon as the wave ends.
+#ifndef PT_RENDER_BLOCK
+#define PT_RENDER_BLOCK 64
+#endif
+constexpr uint32_t kRenderBlock = PT_RENDER_BLOCK;
 template <bool FORCE64, bool COUNT, bool BVH>
 // 4 waves/SIMD (<= 128 VGPRs, a little scratch spill outside the triangle
 // loops): 9.5 ms vs 10.8 ms at 3 waves and 15.3 ms at 2 on the 512^2 x 64spp
@@ -188,14 +197,14 @@ template <bool FORCE64, bool COUNT, bool BVH>
 #ifndef PT_RENDER_WAVES
 #define PT_RENDER_WAVES 4
 #endif
-__global__ __launch_bounds__(256, PT_RENDER_WAVES) void k_render(SceneK S, RenderK R, void* __restrict__ out,
-                                                StatsDev* __restrict__ st) {
-    __shared__ double spill[kSpillSlots][256];
-    const Spill sp{&spill[0][threadIdx.x], 256};
+__global__ __launch_bounds__(kRenderBlock, PT_RENDER_WAVES) void k_render(SceneK S, RenderK R, void* __restrict__ out,
+                                                         StatsDev* __restrict__ st) {
+    __shared__ double spill[kSpillSlots][kRenderBlock];
+    const Spill sp{&spill[0][threadIdx.x], (int)kRenderBlock};
     PT_STAMP(k0);
     // (slot_job's mapping written out: the register allocation of this kernel
     // is sensitive to what stays live across the render loop)
-    const uint32_t tid = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t tid = blockIdx.x * kRenderBlock + threadIdx.x;
     const bool tail = tid >= R.tail_lane;   // wave-uniform
     const uint32_t slog = tail ? R.tail_log2 : R.split_log2, split = 1u << slog;
     const uint32_t lt = tail ? tid - R.tail_lane : tid;
@@ -1260,7 +1269,8 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     // events): order this one after the previous launch, whatever stream
     // that one ran on
     if (s->timed) HIPCHK(hipStreamWaitEvent(st, s->ev1, 0));
-    const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+    const dim3 grid((unsigned)((threads + 255) / 256)), block(256);   // (the wavefront's slots)
+    const dim3 rgrid((unsigned)((threads + kRenderBlock - 1) / kRenderBlock)), rblock(kRenderBlock);
     const bool count = (p->flags & PT_FLAG_COUNT) != 0;
     const bool f64 = (p->flags & PT_FLAG_FORCE_F64) != 0;
     // BVH scenes render through the wavefront kernels unless the caller asks
@@ -1275,14 +1285,14 @@ int pt_render_device(pt_scene* s, const pt_render_params* p, void* out_dev, void
     if (count) HIPCHK(hipMemsetAsync(s->stats, 0, sizeof(StatsDev), st));
     HIPCHK(hipEventRecord(s->ev0, st));
     if (f64) {
-        if (count) hipLaunchKernelGGL((k_render<true, true, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
-        else hipLaunchKernelGGL((k_render<true, false, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+        if (count) hipLaunchKernelGGL((k_render<true, true, true>), rgrid, rblock, 0, st, s->dev, R, out_dev, s->stats);
+        else hipLaunchKernelGGL((k_render<true, false, true>), rgrid, rblock, 0, st, s->dev, R, out_dev, s->stats);
     } else if (s->dev.n_bnode > 0) {   // scenes with meshes: the BVH instantiation
-        if (count) hipLaunchKernelGGL((k_render<false, true, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
-        else hipLaunchKernelGGL((k_render<false, false, true>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+        if (count) hipLaunchKernelGGL((k_render<false, true, true>), rgrid, rblock, 0, st, s->dev, R, out_dev, s->stats);
+        else hipLaunchKernelGGL((k_render<false, false, true>), rgrid, rblock, 0, st, s->dev, R, out_dev, s->stats);
     } else {
-        if (count) hipLaunchKernelGGL((k_render<false, true, false>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
-        else hipLaunchKernelGGL((k_render<false, false, false>), grid, block, 0, st, s->dev, R, out_dev, s->stats);
+        if (count) hipLaunchKernelGGL((k_render<false, true, false>), rgrid, rblock, 0, st, s->dev, R, out_dev, s->stats);
+        else hipLaunchKernelGGL((k_render<false, false, false>), rgrid, rblock, 0, st, s->dev, R, out_dev, s->stats);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(s->ev1, st));
