@@ -1535,6 +1535,33 @@ int pt_image_u8_device(const void* fb_dev, int32_t width, int32_t height, uint32
     if (width <= 0 || height <= 0) return fail(PT_EINVAL, "need width, height > 0");
     const int64_t n = (int64_t)width * height * 3;
     hipStream_t st = (hipStream_t)stream;
+#ifndef PT_IMAGE_V2
+#define PT_IMAGE_V2 1
+#endif
+    if (PT_IMAGE_V2) {   // pt_image.h: per-block partials, no atomics and no fills
+        const int vec = ((uintptr_t)fb_dev % 16 == 0) && ((uintptr_t)out_u8_dev % 4 == 0);
+        const int pblocks = (int)std::max<int64_t>(1, std::min<int64_t>((n / 4 + 255) / 256, kImgBlocks));
+#ifndef PT_IMG_U8_BLOCKS
+#define PT_IMG_U8_BLOCKS 2048
+#endif
+        const int ublocks = (int)std::max<int64_t>(1, std::min<int64_t>((n / 16 + 255) / 256, PT_IMG_U8_BLOCKS));
+        double* part = nullptr;
+        HIPCHK(hipMallocAsync((void**)&part, 2 * sizeof(double) * (size_t)pblocks, st));
+        if (flags & PT_FLAG_OUT_F64) {
+            hipLaunchKernelGGL(k_minmax2<double>, dim3(pblocks), dim3(256), 0, st, (const double*)fb_dev, n, vec,
+                               part);
+            hipLaunchKernelGGL(k_to_u8_2<double>, dim3(ublocks), dim3(256), 0, st, (const double*)fb_dev, n, vec,
+                               part, pblocks, (uint8_t*)out_u8_dev);
+        } else {
+            hipLaunchKernelGGL(k_minmax2<float>, dim3(pblocks), dim3(256), 0, st, (const float*)fb_dev, n, vec,
+                               part);
+            hipLaunchKernelGGL(k_to_u8_2<float>, dim3(ublocks), dim3(256), 0, st, (const float*)fb_dev, n, vec,
+                               part, pblocks, (uint8_t*)out_u8_dev);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipFreeAsync(part, st));
+        return PT_OK;
+    }
     unsigned long long* keys = nullptr;
     HIPCHK(hipMallocAsync((void**)&keys, 2 * sizeof(unsigned long long), st));
     HIPCHK(hipMemsetAsync(keys, 0xff, sizeof(unsigned long long), st));

@@ -3,7 +3,8 @@
 // array, shift, divide by the shifted maximum, x255, truncation to uint8.
 //
 // Two passes over the framebuffer (HBM-bound: 2 reads of 12 B (f32) or
-// 24 B (f64) per pixel + a 3 B write):
+// 24 B (f64) per pixel + a 3 B write).  Version 1 (PT_IMAGE_V2=0; version 2
+// below is the default):
 //   k_minmax  grid-stride reduction; each block folds its min/max into two
 //             64-bit keys with one atomicMin/atomicMax (an order-preserving
 //             map of the doubles, so the result is exact and independent of
@@ -123,6 +124,140 @@ __global__ __launch_bounds__(256) void k_to_u8(const T* __restrict__ fb, int64_t
     }
     for (int64_t i = 4 * n4 + gid; i < n; i += stride)
         out[i] = (uint8_t)to_u8(load_f64(fb, i), mn, mx, nan);
+}
+
+// ---- version 2 (PT_IMAGE_V2, the default): no atomics, no fills --------
+// k_minmax2  per-block min / max in the input type, NaN-propagating
+//            (IEEE minimum/maximum: any NaN in the frame reaches the result),
+//            four 16-byte loads in flight per lane and step (the one-load
+//            loop above ran latency-bound at ~2.9 TB/s), one partial pair per
+//            block into `part` (written by every block: no initialisation);
+// k_to_u8_2  each block first folds the partials (<= kImgBlocks pairs, from
+//            L2), then k_to_u8's element formula, four 4-element groups per
+//            lane and step (2 or 4, 512 to 2048 blocks: within 1%; a
+//            division-free form of the formula with an exact fallback near
+//            integers did not move it either: the pass is memory-bound).
+// min / max of f32 values taken in f32 are the f64 min / max of the same
+// values (the conversion is exact and monotone).
+constexpr int kImgBlocks = 1024;   // k_minmax2's grid at most (4 blocks per CU)
+
+template <typename T>
+__device__ __forceinline__ T nmin(T a, T b) { return __builtin_elementwise_minimum(a, b); }
+template <typename T>
+__device__ __forceinline__ T nmax(T a, T b) { return __builtin_elementwise_maximum(a, b); }
+
+// 4 consecutive elements in their own type (16 B for f32, 32 B for f64)
+__device__ __forceinline__ void load4t(const float* p, int64_t i, float v[4]) {
+    const float4 f = reinterpret_cast<const float4*>(p)[i];
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+}
+__device__ __forceinline__ void load4t(const double* p, int64_t i, double v[4]) {
+    const double2 a = reinterpret_cast<const double2*>(p)[2 * i];
+    const double2 b = reinterpret_cast<const double2*>(p)[2 * i + 1];
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+}
+
+template <typename T>
+__device__ __forceinline__ void fold4(const T v[4], T* mn, T* mx) {
+    *mn = nmin(*mn, nmin(nmin(v[0], v[1]), nmin(v[2], v[3])));
+    *mx = nmax(*mx, nmax(nmax(v[0], v[1]), nmax(v[2], v[3])));
+}
+
+// part[2b] = block b's minimum, part[2b + 1] its maximum (as doubles)
+template <typename T>
+__global__ __launch_bounds__(256) void k_minmax2(const T* __restrict__ fb, int64_t n, int vec,
+                                                 double* __restrict__ part) {
+    T mn = (T)INFINITY, mx = (T)-INFINITY;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n4 = vec ? n / 4 : 0;
+    int64_t i = gid;
+    for (; i + 3 * stride < n4; i += 4 * stride) {   // four groups in flight
+        T a[4], b[4], c[4], d[4];
+        load4t(fb, i, a);
+        load4t(fb, i + stride, b);
+        load4t(fb, i + 2 * stride, c);
+        load4t(fb, i + 3 * stride, d);
+        fold4(a, &mn, &mx);
+        fold4(b, &mn, &mx);
+        fold4(c, &mn, &mx);
+        fold4(d, &mn, &mx);
+    }
+    for (; i < n4; i += stride) {
+        T a[4];
+        load4t(fb, i, a);
+        fold4(a, &mn, &mx);
+    }
+    for (int64_t j = 4 * n4 + gid; j < n; j += stride) {
+        mn = nmin(mn, fb[j]);
+        mx = nmax(mx, fb[j]);
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        mn = nmin(mn, (T)__shfl_xor(mn, m));
+        mx = nmax(mx, (T)__shfl_xor(mx, m));
+    }
+    __shared__ T smin[4], smax[4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { smin[w] = mn; smax[w] = mx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = (double)nmin(nmin(smin[0], smin[1]), nmin(smin[2], smin[3]));
+        part[2 * blockIdx.x + 1] = (double)nmax(nmax(smax[0], smax[1]), nmax(smax[2], smax[3]));
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_to_u8_2(const T* __restrict__ fb, int64_t n, int vec,
+                                                 const double* __restrict__ part, int n_part,
+                                                 uint8_t* __restrict__ out) {
+    __shared__ double smin[4], smax[4];
+    double pmn = INFINITY, pmx = -INFINITY;
+    for (int j = threadIdx.x; j < n_part; j += 256) {
+        pmn = nmin(pmn, part[2 * j]);
+        pmx = nmax(pmx, part[2 * j + 1]);
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        pmn = nmin(pmn, __shfl_xor(pmn, m));
+        pmx = nmax(pmx, __shfl_xor(pmx, m));
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { smin[w] = pmn; smax[w] = pmx; }
+    __syncthreads();
+    const double vmin = nmin(nmin(smin[0], smin[1]), nmin(smin[2], smin[3]));
+    const double vmax = nmax(nmax(smax[0], smax[1]), nmax(smax[2], smax[3]));
+    const bool nan = !(vmin == vmin) || !(vmax == vmax);
+    const double mn = vmin;
+    const double mx = vmax - mn;   // np.max(mat - min) = fl(max - min)
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n4 = vec ? n / 4 : 0;
+    int64_t i = gid;
+#ifndef PT_IMG_U8_DEPTH
+#define PT_IMG_U8_DEPTH 4
+#endif
+    constexpr int D = PT_IMG_U8_DEPTH;   // groups in flight per lane
+    for (; i + (D - 1) * stride < n4; i += D * stride) {
+        T a[D][4];
+#pragma unroll
+        for (int g = 0; g < D; ++g) load4t(fb, i + g * stride, a[g]);
+#pragma unroll
+        for (int g = 0; g < D; ++g) {
+            uint32_t wa = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wa |= to_u8((double)a[g][j], mn, mx, nan) << (8 * j);
+            reinterpret_cast<uint32_t*>(out)[i + g * stride] = wa;
+        }
+    }
+    for (; i < n4; i += stride) {
+        T a[4];
+        load4t(fb, i, a);
+        uint32_t wa = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wa |= to_u8((double)a[j], mn, mx, nan) << (8 * j);
+        reinterpret_cast<uint32_t*>(out)[i] = wa;
+    }
+    for (int64_t j = 4 * n4 + gid; j < n; j += stride)
+        out[j] = (uint8_t)to_u8((double)fb[j], mn, mx, nan);
 }
 
 // Frame assembly of an interleaved multi-GPU render (the step after the

@@ -72,6 +72,35 @@ def test_image_u8_edge_cases():
     c = np.zeros((4, 4, 3))
     c[1, 1, 1] = 1e-300                                        # denormal-scale range
     assert np.array_equal(image_u8(c), _numpy_u8(c))
+    for dt in (np.float64, np.float32):   # 63 elements: 15 vector groups + a 3-element tail
+        d = np.linspace(-1, 1, 7 * 3 * 3).reshape(7, 3, 3).astype(dt)
+        d[-1, -1, -1] = np.nan                                  # NaN in the scalar tail
+        assert np.array_equal(image_u8(d), _numpy_u8(d)), dt
+        e = np.linspace(-1, 1, 7 * 3 * 3).reshape(7, 3, 3).astype(dt)
+        e[2, 1, 0] = -np.inf                                    # -inf minimum: inf - (-inf) paths
+        assert np.array_equal(image_u8(e), _numpy_u8(e)), dt
+        e[5, 2, 2] = np.inf
+        assert np.array_equal(image_u8(e), _numpy_u8(e)), dt
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_image_u8_integer_boundaries(dtype):
+    """Values whose scaled form lands on or next to an integer (k / 255 of the
+    range, and their float neighbours): where the kernel's division-free form
+    must defer to the exact division, since fl(fl(d / m) 255) truncates to
+    k - 1 for some of them."""
+    k = np.arange(256, dtype=np.float64)
+    cols = []
+    for lo, span in ((0.0, 255.0), (-0.37, 1.0), (3.0, 1e-3), (-2.5, 7.3)):
+        v = (lo + span * k / 255.0).astype(dtype)
+        cols += [v, np.nextafter(v, np.inf), np.nextafter(v, -np.inf)]
+    a = np.concatenate(cols)
+    a = a[: (a.size // 3) * 3].reshape(-1, 1, 3)
+    for lo, span in ((0.0, 255.0), (-0.37, 1.0), (3.0, 1e-3), (-2.5, 7.3)):
+        b = a.copy()
+        b[0, 0, 0] = dtype(lo)
+        b[-1, 0, 2] = dtype(lo + span)   # the range the k / 255 points sit on
+        assert np.array_equal(image_u8(b), _numpy_u8(b)), (lo, span)
 
 
 def test_image_u8_large_f32():
