@@ -180,6 +180,29 @@ PT_HD uint32_t wf_start(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfC
 
 // The body of render_lane's loop up to its walks: RNG, light samples, next
 // ray, the fused pass over the uniform units (pt_path.h render_lane).
+// The sort key of a query origin (the BVH frame, PT_WF_BIN, render_wavefront):
+// 4 bits per axis over the root node's grid, in Morton order (neighbouring
+// cells get neighbouring keys)
+PT_HD uint32_t wf_cell(const SceneK& S, F3 o) {
+    if (S.qroot < 0) return 0;
+    const QNode& Q = S.qnode[S.qroot];
+    const float v[3] = {o.x, o.y, o.z};
+    uint32_t c[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float f = (v[a] - Q.org[a]) * (16.0f / (255.0f * q_step(Q.ex, a)));
+        const int i = (int)f;
+        c[a] = (uint32_t)(f > 0.0f ? (i > 15 ? 15 : i) : 0);
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) m |= ((c[a] >> b) & 1u) << (3 * b + a);
+    return m;
+}
+// KEY: the origin's cell in bits 16..27 of the result (k_wf_shade takes it off)
+template <bool KEY = false>
 PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfShadowQ* shq,
                                WfClosestQ* cq) {
     const Spill sp{W->sp, 1};
@@ -248,7 +271,7 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
                                 nullptr);
         }
     }
-    uint32_t want = 0;
+    uint32_t want = KEY ? wf_cell(S, o32) << 16 : 0u;
     wf_put_shadow(shq, o32, ogrp, sh);
     want |= shadow_open<false>(S, &sh);   // the rays still open, one walk each
     if (trace) {
@@ -352,9 +375,10 @@ PT_HD bool wf_finish(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, const 
 // queries wanted.  (One call site of wf_begin_bounce: round 4 started the
 // next bounce from two, inlined twice — 141 instead of 113 VGPRs for
 // k_wf_shade, the same time)
+template <bool KEY = false>
 PT_HD uint32_t wf_shade(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfShadowQ* shq,
                         WfClosestQ* cq, const WfClosestQ* pq) {
-    return wf_finish(S, J, d0, W, shq, cq, pq) ? wf_begin_bounce(S, J, W, shq, cq) : 0u;
+    return wf_finish(S, J, d0, W, shq, cq, pq) ? wf_begin_bounce<KEY>(S, J, W, shq, cq) : 0u;
 }
 
 }  // namespace pt
