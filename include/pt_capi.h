@@ -167,10 +167,8 @@ int pt_band_rows(const pt_render_params* p, int32_t* rows);
 /* Whole loop main.py:186-280 for the selected rows.  out_rgb_dev is a DEVICE
  * pointer (rows*width*3 float32, or float64 with PT_FLAG_OUT_F64), written on
  * `stream` (a hipStream_t, or NULL for the null stream).  Asynchronous unless
- * stats are requested with PT_FLAG_COUNT, except that a BVH scene's wavefront
- * render waits on the host for each step's shade kernel (it sizes the sort of
- * that step's shadow list; the rest of the step stays queued);
- * pt_last_kernel_ms() reads the HIP-event time of the most recent launch. */
+ * stats are requested with PT_FLAG_COUNT; pt_last_kernel_ms() reads the
+ * HIP-event time of the most recent launch. */
 int pt_render_device(pt_scene* scene, const pt_render_params* p,
                      void* out_rgb_dev, void* stream, pt_stats* stats);
 

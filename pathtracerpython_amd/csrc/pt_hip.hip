@@ -21,18 +21,16 @@
 #include "pt_path.h"
 #include "pt_wavefront.h"
 // PT_WF_BIN: the shadow walks' query list sorted by the origin's cell
-// (wf_cell, 8 of its 12 Morton bits: one radix pass) before each walk step
-// (render_wavefront): lanes of a wave then walk from nearby origins toward
-// the light, and the shadow walks run 9% faster.
-// The closest list stays unsorted (random directions: its walks did not gain).
+// (wf_cell, 12 Morton bits; a counting sort on the device, k_bin_hist /
+// k_bin_scatter) before each walk step (render_wavefront): lanes of a wave
+// then walk from nearby origins toward the light, and the shadow walks run
+// 10% faster.  The closest list stays unsorted
+// (random directions: its walks did not gain).
 #ifndef PT_WF_BIN
 #define PT_WF_BIN 1
 #endif
-#ifndef PT_WF_BIN_LO
-#define PT_WF_BIN_LO 4        // the sort's lowest key bit (0: all 12 bits, two passes)
-#endif
 #if PT_WF_BIN
-#include <hipcub/hipcub.hpp>
+#include <hipcub/hipcub.hpp>   // (DeviceScan of the sort's count matrix)
 #endif
 #include "pt_prepare.h"
 #include "pt_image.h"
@@ -382,6 +380,43 @@ __device__ __forceinline__ void wf_append_block(uint32_t want, int32_t* counters
         }
     if (want & kWfWantClosest) closest_list[bc + (int32_t)lanes_below(mc)] = slot;
 }
+// PT_WF_BIN: the shadow list's counting sort on the 12-bit cell key without
+// the host: the list's length is read on the device.  kBinBlocks
+// blocks each take a contiguous chunk of the list; k_bin_hist counts its
+// keys per cell (LDS), a device scan of the cell-major count matrix gives
+// each (cell, block) its output range, and k_bin_scatter places the chunk's
+// entries in their ranges (LDS cursors): every entry lands exactly once.
+constexpr int kBinBits = 12, kBins = 1 << kBinBits, kBinBlocks = 1024;
+__device__ __forceinline__ void bin_chunk(const int32_t* count, int32_t* b0, int32_t* b1) {
+    const int32_t n = *count;
+    const int32_t chunk = (n + kBinBlocks - 1) / kBinBlocks;
+    *b0 = min(n, (int32_t)blockIdx.x * chunk);
+    *b1 = min(n, *b0 + chunk);
+}
+__global__ __launch_bounds__(256) void k_bin_hist(const uint16_t* __restrict__ keys, const int32_t* count,
+                                                  uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kBins];
+    for (int i = threadIdx.x; i < kBins; i += 256) h[i] = 0u;
+    __syncthreads();
+    int32_t b0, b1;
+    bin_chunk(count, &b0, &b1);
+    for (int32_t i = b0 + (int32_t)threadIdx.x; i < b1; i += 256) atomicAdd(&h[keys[i] & (kBins - 1)], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kBins; i += 256) hist[(size_t)i * kBinBlocks + blockIdx.x] = h[i];
+}
+__global__ __launch_bounds__(256) void k_bin_scatter(const uint16_t* __restrict__ keys,
+                                                     const int32_t* __restrict__ vals, const int32_t* count,
+                                                     const uint32_t* __restrict__ off,
+                                                     int32_t* __restrict__ out) {
+    __shared__ uint32_t cur[kBins];
+    for (int i = threadIdx.x; i < kBins; i += 256) cur[i] = off[(size_t)i * kBinBlocks + blockIdx.x];
+    __syncthreads();
+    int32_t b0, b1;
+    bin_chunk(count, &b0, &b1);
+    for (int32_t i = b0 + (int32_t)threadIdx.x; i < b1; i += 256)
+        out[atomicAdd(&cur[keys[i] & (kBins - 1)], 1u)] = vals[i];
+}
+
 // Next list positions for the lanes that need one.  A wave claims a chunk of
 // kWfChunk consecutive positions with one atomic on the list head and hands
 // them out to its lanes as they need work; it claims the next chunk only when
@@ -756,7 +791,6 @@ struct pt_scene {
     hipStream_t wf_side = nullptr;             // the closest walks run beside the shadow walks
     hipEvent_t wf_ev_shade = nullptr, wf_ev_walk = nullptr;
     std::vector<hipEvent_t> prof_ev;           // PT_FLAG_KERNEL_TIMES
-    int32_t* wf_hcnt = nullptr;                // PT_WF_BIN: the list counts, page-locked
 };
 
 namespace {
@@ -851,7 +885,6 @@ void pt_scene_destroy(pt_scene* s) {
         if (s->stats) (void)hipFree(s->stats);
         if (s->out_dev) (void)hipFree(s->out_dev);
         if (s->wf) (void)hipFree(s->wf);
-        if (s->wf_hcnt) (void)hipHostFree(s->wf_hcnt);
         if (s->wf_ev_shade) (void)hipEventDestroy(s->wf_ev_shade);
         if (s->wf_ev_walk) (void)hipEventDestroy(s->wf_ev_walk);
         if (s->wf_side) (void)hipStreamDestroy(s->wf_side);
@@ -1101,18 +1134,20 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     const size_t off_os = off_n + 256, off_ocr = off_os + sz_os, off_ocd = off_ocr + sz_ocr;
     const size_t sz_p = (size_t)R.npix * sizeof(WfClosestQ);   // the primary queries, per pixel
     const size_t off_p = (off_ocd + sz_ocd + 255) / 256 * 256;
-    // PT_WF_BIN: the shadow list's keys and their sorted copy (3 slots x
-    // u16 each), the sorted list (3 slots x i32), the sort's temporary storage
+    // PT_WF_BIN: the shadow list's keys (3 slots x u16), the sorted list
+    // (3 slots x i32), the sort's count matrix, its scan and scan storage
     size_t sz_tmp = 0;
 #if PT_WF_BIN
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sz_tmp, (const uint16_t*)nullptr, (uint16_t*)nullptr,
-                                              (const int32_t*)nullptr, (int32_t*)nullptr, (int)(3 * slots),
-                                              PT_WF_BIN_LO, 12, st));
+    // the count matrix, its scan, the scan's temporary storage
+    size_t sz_scan = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, sz_scan, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                            kBins * kBinBlocks, st));
+    sz_tmp = 2 * (size_t)kBins * kBinBlocks * sizeof(uint32_t) + 256 + sz_scan;
 #endif
-    const size_t sz_k = PT_WF_BIN ? 3 * slots * sizeof(uint16_t) : 0, sz_ko = sz_k,
+    const size_t sz_k = PT_WF_BIN ? 3 * slots * sizeof(uint16_t) : 0,
                  sz_lo = PT_WF_BIN ? 3 * slots * sizeof(int32_t) : 0;
-    const size_t off_k = (off_p + sz_p + 255) / 256 * 256, off_ko = (off_k + sz_k + 255) / 256 * 256,
-                 off_lo = (off_ko + sz_ko + 255) / 256 * 256, off_t = (off_lo + sz_lo + 255) / 256 * 256;
+    const size_t off_k = (off_p + sz_p + 255) / 256 * 256, off_lo = (off_k + sz_k + 255) / 256 * 256,
+                 off_t = (off_lo + sz_lo + 255) / 256 * 256;
     const size_t need = off_t + sz_tmp + 256;
     if (need > s->wf_bytes) {
         if (s->wf) (void)hipFree(s->wf);
@@ -1139,11 +1174,25 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     uint16_t* keys = PT_WF_BIN ? (uint16_t*)(b + off_k) : nullptr;
     int32_t* lists_o = (int32_t*)(b + off_lo);
 #if PT_WF_BIN
-    uint16_t* keys_o = (uint16_t*)(b + off_ko);
-    void* sort_tmp = b + off_t;
-    if (!s->wf_hcnt) HIPCHK(hipHostMalloc((void**)&s->wf_hcnt, 4 * sizeof(int32_t), hipHostMallocDefault));
+    uint32_t* bin_hist = (uint32_t*)(b + off_t);
+    uint32_t* bin_off = bin_hist + (size_t)kBins * kBinBlocks;
+    void* scan_tmp = (char*)(bin_off + (size_t)kBins * kBinBlocks) + 256;
 #endif
     bool sorted = false;   // this step's lists are in lists_o
+#if PT_WF_BIN
+    auto bin_sort = [&]() -> hipError_t {   // (the device reads the list's length: no host wait)
+        hipLaunchKernelGGL(k_bin_hist, dim3(kBinBlocks), dim3(256), 0, st, (const uint16_t*)keys,
+                           (const int32_t*)counters, bin_hist);
+        size_t tb = sz_tmp;
+        const hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, (const uint32_t*)bin_hist, bin_off,
+                                                              kBins * kBinBlocks, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_bin_scatter, dim3(kBinBlocks), dim3(256), 0, st, (const uint16_t*)keys,
+                           (const int32_t*)lists, (const int32_t*)counters, (const uint32_t*)bin_off, lists_o);
+        sorted = true;
+        return hipGetLastError();
+    };
+#endif
     const int32_t per_slot = (R.spp + (int32_t)R.split - 1) / (int32_t)R.split;
     const int32_t steps = per_slot * R.bounces + 2;
     const bool wcount = (flags & PT_FLAG_WALK_COUNT) != 0 && stats;
@@ -1214,19 +1263,9 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
             HIPCHK(mark(step, 2, 1, cs));
             if (side) HIPCHK(hipEventRecord(s->wf_ev_walk, s->wf_side));
 #if PT_WF_BIN
-            // the shadow list sorted by the origin's cell while the closest
-            // walks (unsorted) already run on the side stream: the host
-            // needs the list's length, so it waits for the shade step here
-            if (step > 0) {   // (step 0's closest list is the primary rays, in pixel order)
-                HIPCHK(hipMemcpyAsync(s->wf_hcnt, counters, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-                HIPCHK(hipStreamSynchronize(st));
-                const int ns = s->wf_hcnt[0];
-                size_t tb = sz_tmp;
-                if (ns > 0)
-                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(sort_tmp, tb, keys, keys_o, lists, lists_o, ns,
-                                                              PT_WF_BIN_LO, 12, st));
-                sorted = true;
-            }
+            // the shadow list sorted by the origin's cell (the device reads
+            // its length) while the closest walks, unsorted, already run
+            if (step > 0) HIPCHK(bin_sort());   // (step 0: the primary rays)
 #endif
             HIPCHK(mark(step, 1, 0, st));
             shadow_walk(st);
