@@ -477,6 +477,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_wf_shade(SceneK S, RenderK R, i
     } else if (step == 0) {   // the primary queries are k_wf_primary's (one per pixel)
         const SlotJob j = slot_job(S, R, tid);
         W[tid].acc[0] = W[tid].acc[1] = W[tid].acc[2] = 0.0;
+        W[tid].put_rkey(j.J);
         W[tid].set(j.valid && j.J.n_samples > 0 && j.J.bounces > 0 ? kWfPrimary : kWfDone, false, 0);
     } else if ((tid >> R.split_log2) < R.npix && W[tid].state() != kWfDone) {
         // (a finished slot costs one load: its job is only built when it runs)
@@ -603,7 +604,7 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
             }
         }
         if (slot >= 0) {
-            const Spill sp{W[slot].sp, 1};
+            const Spill sp{W[slot].sp, 1, PT_WF_LRNG != 0};
             if (COUNT)
                 c_units += (pl != kNoRef ? leaf_units(pl) : 0u) + (pl2 != kNoRef ? leaf_units(pl2) : 0u) +
                            (T.ref <= -2 ? leaf_units(T.ref) : 0u);
@@ -685,7 +686,7 @@ __global__ __launch_bounds__(256, PT_CLOSEST_WAVES) void k_wf_closest(SceneK S, 
             }
         }
         if (slot >= 0) {
-            const Spill sp{W[(size_t)slot << wshift].sp, 1};
+            const Spill sp{W[(size_t)slot << wshift].sp, 1, PT_WF_LRNG != 0};
             if (COUNT)
                 c_units += (pl != kNoRef ? leaf_units(pl) : 0u) + (pl2 != kNoRef ? leaf_units(pl2) : 0u) +
                            (T.ref <= -2 ? leaf_units(T.ref) : 0u);

@@ -51,12 +51,24 @@ PT_HD void bump(Counters* c, uint32_t Counters::*f, uint32_t v) {
 struct Spill {
     double* base;
     int stride;
+    // wf: the home is a wavefront path record (pt_wavefront.h WfPath), which
+    // keeps no light points: shadow_setup_k does not store them and light()
+    // draws them again from the slot's RNG key (the record's light-point
+    // slots hold that key, WfPath::put_rkey).  Writing the points into the
+    // record's second line cost the shade step 13% (a partial-line write per
+    // slot and bounce); the rare f64 blocks that need a point redraw it.
+    bool wf = false;   // (the wavefront sets it to PT_WF_LRNG)
     PT_HD double get(int i) const { return base[i * stride]; }
     PT_HD void put(int i, double v) const { base[i * stride] = v; }
     PT_HD D3 get3(int i) const { return d3(get(i), get(i + 1), get(i + 2)); }
     PT_HD void put3(int i, D3 v) const { put(i, v.x); put(i + 1, v.y); put(i + 2, v.z); }
+    template <class Sc>
+    PT_HD D3 light(const Sc& S, int k) const;
 };
 constexpr int kSpillSlots = 20;
+#ifndef PT_WF_LRNG
+#define PT_WF_LRNG 1   // the wavefront's records keep no light points (Spill::wf)
+#endif
 // P and Nd first: the wavefront path record (pt_wavefront.h WfPath) keeps them
 // in the same 128-B line as the per-step fields; the light points and the
 // primary hit follow in the other line
@@ -259,7 +271,7 @@ PT_HD void shadow_setup_k(const SceneK& S, D3 P, D3 n, int k, double u0, double 
                           double u3, ShadowSet* sh, const Spill& sp) {
     const int li = pick_light(S, u0);
     const D3 L = light_point(S.trid[S.light_tri[li]], u1, u2, u3);
-    sp.put3(kSpL + 3 * k, L);
+    if (!sp.wf) sp.put3(kSpL + 3 * k, L);
     const D3 dn = unit(L - P);                    // main.py:37-38
     const float tl = sqrtf((float)squared_dist(P, L));   // main.py:40, to ~2e-7
     sh->hlo[k] = tl * (1.0f - 1e-6f);
@@ -277,6 +289,36 @@ PT_HD void shadow_setup(const SceneK& S, D3 P, D3 n, const double u[12], ShadowS
         shadow_setup_k<COUNT>(S, P, n, k, u[4 * k], u[4 * k + 1], u[4 * k + 2], u[4 * k + 3], sh, sp);
     sh->key2 = COUNT ? S.n_tri : S.n_obj;
     sh->leak = S.n_obj - 1;
+}
+// light sample k of the path's current bounce drawn again from its RNG key,
+// with shadow_setup_k's operations (bit for bit its L)
+PT_HD D3 light_redraw(const SceneK& S, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t b, int k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // (the launch's seed, the same in every lane: rng_block keys from SGPRs)
+    seed = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(seed >> 32)) << 32) |
+           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)seed);
+#endif
+    uint32_t c[4];
+    rng_block(seed, pixel, sample, b, (uint32_t)k, c);
+    const int li = pick_light(S, u_of(c[0]));
+    return light_point(S.trid[S.light_tri[li]], u_of(c[1]), u_of(c[2]), u_of(c[3]));
+}
+// the wavefront record's RNG key in its light-point slots (written once per
+// slot, k_wf_shade step 0): the seed, pixel | sample0 << 32, the sample stride;
+// the sample index and the bounce are the record's si and sb, just below
+// the home (offsets checked in pt_wavefront.h)
+template <class Sc>
+PT_HD D3 Spill::light(const Sc& S, int k) const {
+    if (!wf) return get3(kSpL + 3 * k);
+    uint64_t w0, w1, w2;
+    const double d0 = get(kSpL), d1 = get(kSpL + 1), d2 = get(kSpL + 2);
+    __builtin_memcpy(&w0, &d0, 8);
+    __builtin_memcpy(&w1, &d1, 8);
+    __builtin_memcpy(&w2, &d2, 8);
+    const int32_t si = reinterpret_cast<const int32_t*>(base)[-2];
+    const uint32_t sb = reinterpret_cast<const uint32_t*>(base)[-1];
+    const uint32_t sample = (uint32_t)((int32_t)(w1 >> 32) + si * (int32_t)w2);
+    return light_redraw(S, w0, (uint32_t)w1, sample, sb >> 3, k);
 }
 
 // Shadow rays of the uniform (scene-order) loop with the filter verdicts as
@@ -503,7 +545,7 @@ PT_HD void fused_fallback(const SceneK& S, const UnitF& U, uint32_t amb, ShadowS
             D3 Q;
             double sqd;
             if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
-            const D3 L = sp.get3(kSpL + 3 * k);
+            const D3 L = sp.light(S, k);
             if (eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
                 sqd < squared_dist(P, L)) {
                 if (COUNT && t < sh->first[k]) sh->first[k] = t;
@@ -1383,7 +1425,7 @@ PT_HD void shadow1_fallback(const SceneK& S, const UnitF& U, bool a0, bool a1, S
                       const Spill& sp) {
     const bool last = r->k == kLightSamples - 1;
     const D3 P = sp.get3(kSpP);
-    const D3 L = sp.get3(kSpL + 3 * r->k);
+    const D3 L = sp.light(S, r->k);
     for (int i = 0; i < 2; ++i) {
         if (!(i == 0 ? a0 : a1)) continue;
         if (last ? (U.obj >= r->key2) : r->occ) continue;   // decided meanwhile

@@ -36,22 +36,32 @@ enum : int32_t { kWfDone = 0, kWfPrimary = 1, kWfBounce = 2, kWfBegin = 3 };
 
 // Two 128-B lines per slot: the first holds everything a shade step reads
 // and writes (the per-step fields and the spill slots P, Nd), the second the
-// light points (written per bounce, read only by f64 fallbacks) and the
-// primary hit (read when a sample restarts).
+// slot's RNG key in the light-point slots (written once; PT_WF_LRNG: the f64
+// fallbacks redraw a light point from it, Spill::light — with PT_WF_LRNG=0
+// the points themselves, written per bounce) and the primary hit (read when
+// a sample restarts).
 struct alignas(128) WfPath {
     double acc[3];            // sum of this slot's sample colours
     double k, kk;             // throughput before / after the pending bounce
     double ln[kLightSamples]; // l_k . n of the pending bounce's light samples
     int32_t tri, tri0, si;    // the pending bounce's triangle, the primary hit's, the sample
     uint32_t sb;              // state | trace << 2 | b << 3 (the bounce index)
-    double sp[kSpillSlots];   // the spill home of pt_path.h (Spill{sp, 1}): P, Nd | L, D0, P0
+    double sp[kSpillSlots];   // the spill home of pt_path.h (Spill{sp, 1, wf}): P, Nd | key (L), D0, P0
     double pad[2];
     PT_HD int state() const { return (int)(sb & 3u); }
     PT_HD bool trace() const { return ((sb >> 2) & 1u) != 0; }
     PT_HD int b() const { return (int)(sb >> 3); }
     PT_HD void set(int state, bool trace, int b) { sb = (uint32_t)state | (trace ? 4u : 0u) | ((uint32_t)b << 3); }
+    // the slot's RNG key in the light-point slots (Spill::light)
+    PT_HD void put_rkey(const LaneJob& J) {
+        const uint64_t w[3] = {J.seed, (uint64_t)J.pixel | (uint64_t)(uint32_t)J.sample0 << 32,
+                               (uint64_t)(uint32_t)J.sample_stride};
+        __builtin_memcpy(&sp[kSpL], w, sizeof(w));
+    }
 };
 static_assert(sizeof(WfPath) == 256, "WfPath is 256 B");
+static_assert(offsetof(WfPath, si) + 8 == offsetof(WfPath, sp) && offsetof(WfPath, sb) + 4 == offsetof(WfPath, sp),
+              "Spill::light reads si and sb just below the home");
 static_assert(offsetof(WfPath, sp) + (kSpNd + 3) * sizeof(double) <= 128,
               "P and Nd in the first line");
 
@@ -160,7 +170,7 @@ PT_HD uint32_t wf_start(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfC
     W->acc[0] = W->acc[1] = W->acc[2] = 0.0;
     W->set(kWfDone, false, 0);
     if (J.n_samples <= 0 || J.bounces <= 0) return 0;   // main.py:192 never runs
-    const Spill sp{W->sp, 1};
+    const Spill sp{W->sp, 1, PT_WF_LRNG != 0};
     const D3 eye = ld3(S.eye);
     const D3 dn = unit(d0);
     sp.put3(kSpP, eye);
@@ -205,7 +215,7 @@ PT_HD uint32_t wf_cell(const SceneK& S, F3 o) {
 template <bool KEY = false>
 PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfShadowQ* shq,
                                WfClosestQ* cq) {
-    const Spill sp{W->sp, 1};
+    const Spill sp{W->sp, 1, PT_WF_LRNG != 0};
     const D3 P = sp.get3(kSpP);
     const int tri = W->tri, b = W->b();
     const uint32_t sample = (uint32_t)(J.sample0 + W->si * J.sample_stride);
@@ -292,7 +302,7 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
 // shares one per pixel, k_wf_primary; the host emulation has one per slot, cq)
 PT_HD bool wf_finish(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, const WfShadowQ* shq,
                      const WfClosestQ* cq, const WfClosestQ* pq) {
-    const Spill sp{W->sp, 1};
+    const Spill sp{W->sp, 1, PT_WF_LRNG != 0};
     if (W->state() == kWfPrimary) {   // k_render: closest(eye, d0) then render_lane's prologue
         D3 P0 = d3(0, 0, 0);
         const int tri0 = closest_finish<false, false, true>(S, wf_get_acc(*pq), ld3(S.eye), unit(d0),
