@@ -604,7 +604,7 @@ __global__ __launch_bounds__(256, PT_SHADOW_WAVES) void k_wf_shadow(SceneK S, Wf
             }
         }
         if (slot >= 0) {
-            const Spill sp{W[slot].sp, 1, PT_WF_LRNG != 0};
+            const Spill sp{W[slot].sp, 1};
             if (COUNT)
                 c_units += (pl != kNoRef ? leaf_units(pl) : 0u) + (pl2 != kNoRef ? leaf_units(pl2) : 0u) +
                            (T.ref <= -2 ? leaf_units(T.ref) : 0u);
@@ -686,7 +686,7 @@ __global__ __launch_bounds__(256, PT_CLOSEST_WAVES) void k_wf_closest(SceneK S, 
             }
         }
         if (slot >= 0) {
-            const Spill sp{W[(size_t)slot << wshift].sp, 1, PT_WF_LRNG != 0};
+            const Spill sp{W[(size_t)slot << wshift].sp, 1};
             if (COUNT)
                 c_units += (pl != kNoRef ? leaf_units(pl) : 0u) + (pl2 != kNoRef ? leaf_units(pl2) : 0u) +
                            (T.ref <= -2 ? leaf_units(T.ref) : 0u);

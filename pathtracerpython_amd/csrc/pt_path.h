@@ -51,23 +51,21 @@ PT_HD void bump(Counters* c, uint32_t Counters::*f, uint32_t v) {
 struct Spill {
     double* base;
     int stride;
-    // wf: the home is a wavefront path record (pt_wavefront.h WfPath), which
-    // keeps no light points: shadow_setup_k does not store them and light()
-    // draws them again from the slot's RNG key (the record's light-point
-    // slots hold that key, WfPath::put_rkey).  Writing the points into the
-    // record's second line cost the shade step 13% (a partial-line write per
-    // slot and bounce); the rare f64 blocks that need a point redraw it.
-    bool wf = false;   // (the wavefront sets it to PT_WF_LRNG)
     PT_HD double get(int i) const { return base[i * stride]; }
     PT_HD void put(int i, double v) const { base[i * stride] = v; }
     PT_HD D3 get3(int i) const { return d3(get(i), get(i + 1), get(i + 2)); }
     PT_HD void put3(int i, D3 v) const { put(i, v.x); put(i + 1, v.y); put(i + 2, v.z); }
-    template <class Sc>
-    PT_HD D3 light(const Sc& S, int k) const;
 };
 constexpr int kSpillSlots = 20;
+// PT_WF_LRNG: a wavefront path record (pt_wavefront.h WfPath) keeps no light
+// points — shadow_setup_k<.., false> does not store them, and the rare f64
+// blocks that need one draw it again from the slot's RNG key (wf_light; the
+// record's light-point slots hold that key, WfPath::put_rkey).  Writing the
+// points into the record's second line cost the shade step 10% (a
+// partial-line write per slot and bounce).  The render kernel's LDS home is
+// unchanged (a compile-time choice: the kernel's code stays as it was).
 #ifndef PT_WF_LRNG
-#define PT_WF_LRNG 1   // the wavefront's records keep no light points (Spill::wf)
+#define PT_WF_LRNG 1
 #endif
 // P and Nd first: the wavefront path record (pt_wavefront.h WfPath) keeps them
 // in the same 128-B line as the per-step fields; the light points and the
@@ -266,12 +264,12 @@ struct ShadowSet {
 // brackets into sh, with l_k . n for the colour.  u: the 12 uniforms (the
 // render loop draws them with rng_blocks4; the batched API passes them in).
 // light sample k of shadow_setup (u: its 4 uniforms)
-template <bool COUNT>
+template <bool COUNT, bool STORE_L = true>
 PT_HD void shadow_setup_k(const SceneK& S, D3 P, D3 n, int k, double u0, double u1, double u2,
                           double u3, ShadowSet* sh, const Spill& sp) {
     const int li = pick_light(S, u0);
     const D3 L = light_point(S.trid[S.light_tri[li]], u1, u2, u3);
-    if (!sp.wf) sp.put3(kSpL + 3 * k, L);
+    if (STORE_L) sp.put3(kSpL + 3 * k, L);
     const D3 dn = unit(L - P);                    // main.py:37-38
     const float tl = sqrtf((float)squared_dist(P, L));   // main.py:40, to ~2e-7
     sh->hlo[k] = tl * (1.0f - 1e-6f);
@@ -306,12 +304,11 @@ PT_HD D3 light_redraw(const SceneK& S, uint64_t seed, uint32_t pixel, uint32_t s
 // the wavefront record's RNG key in its light-point slots (written once per
 // slot, k_wf_shade step 0): the seed, pixel | sample0 << 32, the sample stride;
 // the sample index and the bounce are the record's si and sb, just below
-// the home (offsets checked in pt_wavefront.h)
-template <class Sc>
-PT_HD D3 Spill::light(const Sc& S, int k) const {
-    if (!wf) return get3(kSpL + 3 * k);
+// the home (offsets checked in pt_wavefront.h).  sp: a wavefront home only.
+PT_HD D3 wf_light(const SceneK& S, const Spill& sp, int k) {
+    const double* base = sp.base;
     uint64_t w0, w1, w2;
-    const double d0 = get(kSpL), d1 = get(kSpL + 1), d2 = get(kSpL + 2);
+    const double d0 = sp.get(kSpL), d1 = sp.get(kSpL + 1), d2 = sp.get(kSpL + 2);
     __builtin_memcpy(&w0, &d0, 8);
     __builtin_memcpy(&w1, &d1, 8);
     __builtin_memcpy(&w2, &d2, 8);
@@ -529,7 +526,7 @@ PT_HD uint32_t shadow_bits_m(const SceneK& S, const UnitF& U, const OriginU& O, 
 // The f64 decisions of a unit's ambiguous tests (bits of amb, see
 // fused_unit): one rare block per unit (an eval64 per bit), entered by few
 // waves.
-template <bool FORCE64, bool COUNT, bool MARGIN, int PARTS = 3>
+template <bool FORCE64, bool COUNT, bool MARGIN, int PARTS = 3, bool LRNG = false>
 PT_HD void fused_fallback(const SceneK& S, const UnitF& U, uint32_t amb, ShadowSet* sh,
                           ClosestAcc* ca, const Spill& sp, Counters* cnt, float* oc) {
     const D3 P = sp.get3(kSpP);
@@ -545,7 +542,7 @@ PT_HD void fused_fallback(const SceneK& S, const UnitF& U, uint32_t amb, ShadowS
             D3 Q;
             double sqd;
             if (!FORCE64) bump<COUNT>(cnt, &Counters::fallbacks, 1);
-            const D3 L = sp.light(S, k);
+            const D3 L = LRNG ? wf_light(S, sp, k) : sp.get3(kSpL + 3 * k);
             if (eval64(S.trid[t], P, unit(L - P), &Q, &sqd) && !(sqd < kZero) &&
                 sqd < squared_dist(P, L)) {
                 if (COUNT && t < sh->first[k]) sh->first[k] = t;
@@ -586,7 +583,7 @@ PT_HD void fused_fallback(const SceneK& S, const UnitF& U, uint32_t amb, ShadowS
 // call site (the walks' leaves test one kind only: the other kind's code,
 // its f64 block included, is then not compiled in — the closest walk
 // kernel ran 21% faster without the dead shadow block)
-template <bool FORCE64, bool COUNT, bool MARGIN = false, int PARTS = 3>
+template <bool FORCE64, bool COUNT, bool MARGIN = false, int PARTS = 3, bool LRNG = false>
 PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
                       bool do_shadow, bool do_closest, ShadowSet* sh, F3 n32, ClosestAcc* ca,
                       const Spill& sp, Counters* cnt, uint32_t rays = 15u,
@@ -669,7 +666,7 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
     if (PT_AMB_MAX && MARGIN && PT_QUAD && (PARTS & 1) && !(amax < 0.0f))   // rare: rebuild the bits
         amb |= shadow_bits_m(S, U, O, coplanar, sh, oc);
     amb &= ((PARTS & 1) ? 0x3fu : 0u) | ((PARTS & 2) ? 0xc0u : 0u);
-    if (amb) fused_fallback<FORCE64, COUNT, MARGIN, PARTS>(S, U, amb, sh, ca, sp, cnt, oc);   // rare (FORCE64: every shadow test) — decide in f64
+    if (amb) fused_fallback<FORCE64, COUNT, MARGIN, PARTS, LRNG>(S, U, amb, sh, ca, sp, cnt, oc);   // rare (FORCE64: every shadow test) — decide in f64
 }
 
 template <bool COUNT>
@@ -1425,7 +1422,7 @@ PT_HD void shadow1_fallback(const SceneK& S, const UnitF& U, bool a0, bool a1, S
                       const Spill& sp) {
     const bool last = r->k == kLightSamples - 1;
     const D3 P = sp.get3(kSpP);
-    const D3 L = sp.light(S, r->k);
+    const D3 L = PT_WF_LRNG ? wf_light(S, sp, r->k) : sp.get3(kSpL + 3 * r->k);   // (the walks' only)
     for (int i = 0; i < 2; ++i) {
         if (!(i == 0 ? a0 : a1)) continue;
         if (last ? (U.obj >= r->key2) : r->occ) continue;   // decided meanwhile

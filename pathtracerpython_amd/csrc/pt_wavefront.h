@@ -46,7 +46,7 @@ struct alignas(128) WfPath {
     double ln[kLightSamples]; // l_k . n of the pending bounce's light samples
     int32_t tri, tri0, si;    // the pending bounce's triangle, the primary hit's, the sample
     uint32_t sb;              // state | trace << 2 | b << 3 (the bounce index)
-    double sp[kSpillSlots];   // the spill home of pt_path.h (Spill{sp, 1, wf}): P, Nd | key (L), D0, P0
+    double sp[kSpillSlots];   // the spill home of pt_path.h (Spill{sp, 1}): P, Nd | key (L), D0, P0
     double pad[2];
     PT_HD int state() const { return (int)(sb & 3u); }
     PT_HD bool trace() const { return ((sb >> 2) & 1u) != 0; }
@@ -170,7 +170,7 @@ PT_HD uint32_t wf_start(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, WfC
     W->acc[0] = W->acc[1] = W->acc[2] = 0.0;
     W->set(kWfDone, false, 0);
     if (J.n_samples <= 0 || J.bounces <= 0) return 0;   // main.py:192 never runs
-    const Spill sp{W->sp, 1, PT_WF_LRNG != 0};
+    const Spill sp{W->sp, 1};
     const D3 eye = ld3(S.eye);
     const D3 dn = unit(d0);
     sp.put3(kSpP, eye);
@@ -215,7 +215,7 @@ PT_HD uint32_t wf_cell(const SceneK& S, F3 o) {
 template <bool KEY = false>
 PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfShadowQ* shq,
                                WfClosestQ* cq) {
-    const Spill sp{W->sp, 1, PT_WF_LRNG != 0};
+    const Spill sp{W->sp, 1};
     const D3 P = sp.get3(kSpP);
     const int tri = W->tri, b = W->b();
     const uint32_t sample = (uint32_t)(J.sample0 + W->si * J.sample_stride);
@@ -230,8 +230,8 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
     for (int k = 0; k < kLightSamples; ++k) {
         uint32_t c[4];
         rng_block(J.seed, J.pixel, sample, (uint32_t)b, (uint32_t)k, c);
-        shadow_setup_k<false>(S, P, ld3(R.n), k, u_of(c[0]), u_of(c[1]), u_of(c[2]), u_of(c[3]),
-                              &sh, sp);
+        shadow_setup_k<false, !PT_WF_LRNG>(S, P, ld3(R.n), k, u_of(c[0]), u_of(c[1]), u_of(c[2]),
+                                           u_of(c[3]), &sh, sp);
     }
     sh.key2 = S.n_obj;
     sh.leak = S.n_obj - 1;
@@ -268,8 +268,8 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
             const UnitF U = S.unit[u];
             const OriginU O = PT_QUAD ? origin_q(U, o32u) : origin_u(U, o32u);
             const bool do_shadow = PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));
-            fused_unit<false, false, true>(S, U, O, U.grp == ogrp, do_shadow, any_trace, &sh, n32,
-                                           &ca, sp, nullptr, 15u, oc);
+            fused_unit<false, false, true, 3, PT_WF_LRNG != 0>(S, U, O, U.grp == ogrp, do_shadow, any_trace,
+                                                               &sh, n32, &ca, sp, nullptr, 15u, oc);
         }
 #pragma unroll
         for (int k = 0; k < kLightSamples; ++k) sh.occ[k] = oc[k] > 0.0f;
@@ -302,7 +302,7 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
 // shares one per pixel, k_wf_primary; the host emulation has one per slot, cq)
 PT_HD bool wf_finish(const SceneK& S, const LaneJob& J, D3 d0, WfPath* W, const WfShadowQ* shq,
                      const WfClosestQ* cq, const WfClosestQ* pq) {
-    const Spill sp{W->sp, 1, PT_WF_LRNG != 0};
+    const Spill sp{W->sp, 1};
     if (W->state() == kWfPrimary) {   // k_render: closest(eye, d0) then render_lane's prologue
         D3 P0 = d3(0, 0, 0);
         const int tri0 = closest_finish<false, false, true>(S, wf_get_acc(*pq), ld3(S.eye), unit(d0),
