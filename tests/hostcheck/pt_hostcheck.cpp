@@ -157,7 +157,10 @@ int hc_render_wavefront2(const pt_scene_desc* d, const pt_render_params* p, doub
         bool any = false;
         for (size_t i = 0; i < n; ++i) {
             want[i] = 0;
-            if (step == 0) want[i] = wf_start(H.k, J[i], D0[i], &W[i], &CQ[i]);
+            if (step == 0) {   // (k_wf_shade's step 0: the slot's RNG key, then k_wf_primary)
+                W[i].put_rkey(J[i]);
+                want[i] = wf_start(H.k, J[i], D0[i], &W[i], &CQ[i]);
+            }
             else if (W[i].state() != kWfDone) {
                 want[i] = wf_shade(H.k, J[i], D0[i], &W[i], &SQ[i], &CQ[i], &CQ[i]);
                 any = true;
