@@ -136,7 +136,14 @@ PT_HD void wf_get_shadow1(const WfShadowQ& q, int k, F3* o32, int* ogrp, Shadow1
     r->leak = q.leak;
 }
 // its result into the query record (fields of ray k only)
+// (only an occluded ray writes: wocc is 0 from wf_put_shadow, and a ray's
+// leak changes only when it is occluded — an unoccluded ray's walk leaves
+// the query record's lines untouched, PT_WF_PUT_OCC)
+#ifndef PT_WF_PUT_OCC
+#define PT_WF_PUT_OCC 1
+#endif
 PT_HD void wf_put_shadow1(WfShadowQ* q, const Shadow1& r) {
+    if (PT_WF_PUT_OCC && !r.occ) return;
     if (r.k < kLightSamples - 1) {
         q->wocc[r.k] = r.occ ? 1 : 0;
     } else {
