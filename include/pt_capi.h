@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 6
+#define PT_API_VERSION 7
 
 /* error codes */
 #define PT_OK 0
@@ -139,6 +139,10 @@ typedef struct pt_stats {
      * and launch count of each wavefront kernel                            */
     double shade_ms, shadow_ms, closest_ms;
     uint64_t shade_launches, shadow_launches, closest_launches;
+    /* (v7) the shadow list's counting sort between the shade and the shadow
+     * walks (its four kernels per step) */
+    double sort_ms;
+    uint64_t sort_launches;
 } pt_stats;
 
 typedef struct pt_scene pt_scene;

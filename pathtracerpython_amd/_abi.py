@@ -1,7 +1,7 @@
 """ctypes mirror of include/pt_capi.h (structs, flags, error codes)."""
 import ctypes as C
 
-PT_API_VERSION = 6
+PT_API_VERSION = 7
 
 PT_OK = 0
 PT_EINVAL = -1
@@ -63,7 +63,8 @@ class PtStats(C.Structure):
         "shadow_queries", "shadow_node_visits", "shadow_leaf_units",
         "closest_queries", "closest_node_visits", "closest_leaf_units")] + \
         [(n, C.c_double) for n in ("shade_ms", "shadow_ms", "closest_ms")] + \
-        [(n, C.c_uint64) for n in ("shade_launches", "shadow_launches", "closest_launches")]
+        [(n, C.c_uint64) for n in ("shade_launches", "shadow_launches", "closest_launches")] + \
+        [("sort_ms", C.c_double), ("sort_launches", C.c_uint64)]
 
     COUNTERS = ("closest_tests", "shadow_tests", "ray_bounces", "shading_points",
                 "light_hits", "escapes", "f64_fallbacks", "f64_rescans")

@@ -30,7 +30,6 @@
 #define PT_WF_BIN 1
 #endif
 #if PT_WF_BIN
-#include <hipcub/hipcub.hpp>   // (DeviceScan of the sort's count matrix)
 #endif
 #include "pt_prepare.h"
 #include "pt_image.h"
@@ -381,38 +380,107 @@ __device__ __forceinline__ void wf_append_block(uint32_t want, int32_t* counters
     if (want & kWfWantClosest) closest_list[bc + (int32_t)lanes_below(mc)] = slot;
 }
 // PT_WF_BIN: the shadow list's counting sort on the 12-bit cell key without
-// the host: the list's length is read on the device.  kBinBlocks
-// blocks each take a contiguous chunk of the list; k_bin_hist counts its
-// keys per cell (LDS), a device scan of the cell-major count matrix gives
-// each (cell, block) its output range, and k_bin_scatter places the chunk's
-// entries in their ranges (LDS cursors): every entry lands exactly once.
-constexpr int kBinBits = 12, kBins = 1 << kBinBits, kBinBlocks = 1024;
-__device__ __forceinline__ void bin_chunk(const int32_t* count, int32_t* b0, int32_t* b1) {
-    const int32_t n = *count;
-    const int32_t chunk = (n + kBinBlocks - 1) / kBinBlocks;
+// the host: the list's length n is read on the device.  nb = bin_cols(n)
+// blocks (at most kBinBlocks, at least kBinMinChunk entries each, so a short
+// list pays a small count matrix) each take a contiguous chunk of the list;
+// k_bin_hist counts its keys per cell (LDS) into the cell-major count matrix
+// (kBins x nb), k_bin_rows turns each cell's row into its exclusive prefix
+// sums in place (one wave per row) and writes the row's total, k_bin_base
+// scans the kBins totals (one block), and k_bin_scatter places the chunk's
+// entries at base[cell] + row prefix (LDS cursors): every entry lands exactly
+// once, in (cell, block, position-in-block) order.  Hand-written two-level
+// scan, no decoupled lookback: a lookback scan's blocks can wait behind the
+// persistent closest-walk blocks that share the GPU (DESIGN.md §11, 13.7 ms
+// per call for hipCUB's).
+constexpr int kBinBits = 12, kBins = 1 << kBinBits, kBinBlocks = 1024, kBinMinChunk = 2048;
+static_assert(kBinBlocks <= 64 * 16, "k_bin_rows: a row is at most 16 entries per lane");
+static_assert(kBins % 4 == 0 && kBins == 4 * 1024, "k_bin_rows: 4 rows per block; k_bin_base: 4 per thread");
+__device__ __forceinline__ int32_t bin_cols(int32_t n) {
+    const int32_t c = (n + kBinMinChunk - 1) / kBinMinChunk;
+    return c < 1 ? 1 : (c > kBinBlocks ? kBinBlocks : c);
+}
+__device__ __forceinline__ void bin_chunk(int32_t n, int32_t nb, int32_t* b0, int32_t* b1) {
+    const int32_t chunk = (n + nb - 1) / nb;
     *b0 = min(n, (int32_t)blockIdx.x * chunk);
     *b1 = min(n, *b0 + chunk);
+}
+// inclusive prefix sum over the 64 lanes of a wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = (int)(threadIdx.x & 63u);
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
 }
 __global__ __launch_bounds__(256) void k_bin_hist(const uint16_t* __restrict__ keys, const int32_t* count,
                                                   uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[kBins];
+    const int32_t n = *count, nb = bin_cols(n);
+    if ((int32_t)blockIdx.x >= nb) return;   // (block-uniform, before any barrier)
     for (int i = threadIdx.x; i < kBins; i += 256) h[i] = 0u;
     __syncthreads();
     int32_t b0, b1;
-    bin_chunk(count, &b0, &b1);
+    bin_chunk(n, nb, &b0, &b1);
     for (int32_t i = b0 + (int32_t)threadIdx.x; i < b1; i += 256) atomicAdd(&h[keys[i] & (kBins - 1)], 1u);
     __syncthreads();
-    for (int i = threadIdx.x; i < kBins; i += 256) hist[(size_t)i * kBinBlocks + blockIdx.x] = h[i];
+    for (int i = threadIdx.x; i < kBins; i += 256) hist[(size_t)i * nb + blockIdx.x] = h[i];
+}
+// kBins / 4 blocks: one row of the count matrix per wave, lane l holding the
+// row's entries [l per, (l + 1) per); the row becomes its exclusive prefix
+// sums, its total goes to rowsum
+__global__ __launch_bounds__(256) void k_bin_rows(uint32_t* __restrict__ hist, const int32_t* count,
+                                                  uint32_t* __restrict__ rowsum) {
+    const int32_t nb = bin_cols(*count);
+    const int row = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
+    uint32_t* r = hist + (size_t)row * nb;
+    const int per = (nb + 63) >> 6;
+    uint32_t v[16], s = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int i = lane * per + j;
+        v[j] = (j < per && i < nb) ? r[i] : 0u;
+        s += v[j];
+    }
+    const uint32_t incl = wave_incl_scan(s);
+    uint32_t x = incl - s;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int i = lane * per + j;
+        if (j < per && i < nb) r[i] = x;
+        x += v[j];
+    }
+    if (lane == 63) rowsum[row] = incl;
+}
+// one block of 1024: the exclusive prefix sums of the kBins row totals
+__global__ __launch_bounds__(1024) void k_bin_base(const uint32_t* __restrict__ rowsum,
+                                                   uint32_t* __restrict__ base) {
+    __shared__ uint32_t wsum[16];
+    const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = rowsum[4 * t + j]; s += v[j]; }
+    const uint32_t incl = wave_incl_scan(s);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t x = incl - s;
+    for (int i = 0; i < w; ++i) x += wsum[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { base[4 * t + j] = x; x += v[j]; }
 }
 __global__ __launch_bounds__(256) void k_bin_scatter(const uint16_t* __restrict__ keys,
                                                      const int32_t* __restrict__ vals, const int32_t* count,
                                                      const uint32_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ base,
                                                      int32_t* __restrict__ out) {
     __shared__ uint32_t cur[kBins];
-    for (int i = threadIdx.x; i < kBins; i += 256) cur[i] = off[(size_t)i * kBinBlocks + blockIdx.x];
+    const int32_t n = *count, nb = bin_cols(n);
+    if ((int32_t)blockIdx.x >= nb) return;   // (block-uniform, before any barrier)
+    for (int i = threadIdx.x; i < kBins; i += 256) cur[i] = base[i] + off[(size_t)i * nb + blockIdx.x];
     __syncthreads();
     int32_t b0, b1;
-    bin_chunk(count, &b0, &b1);
+    bin_chunk(n, nb, &b0, &b1);
     for (int32_t i = b0 + (int32_t)threadIdx.x; i < b1; i += 256)
         out[atomicAdd(&cur[keys[i] & (kBins - 1)], 1u)] = vals[i];
 }
@@ -1139,11 +1207,8 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     // (3 slots x i32), the sort's count matrix, its scan and scan storage
     size_t sz_tmp = 0;
 #if PT_WF_BIN
-    // the count matrix, its scan, the scan's temporary storage
-    size_t sz_scan = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, sz_scan, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                            kBins * kBinBlocks, st));
-    sz_tmp = 2 * (size_t)kBins * kBinBlocks * sizeof(uint32_t) + 256 + sz_scan;
+    // the count matrix (its rows' prefix sums in place), the row totals and their scan
+    sz_tmp = ((size_t)kBins * kBinBlocks + 2 * (size_t)kBins) * sizeof(uint32_t);
 #endif
     const size_t sz_k = PT_WF_BIN ? 3 * slots * sizeof(uint16_t) : 0,
                  sz_lo = PT_WF_BIN ? 3 * slots * sizeof(int32_t) : 0;
@@ -1176,20 +1241,20 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     int32_t* lists_o = (int32_t*)(b + off_lo);
 #if PT_WF_BIN
     uint32_t* bin_hist = (uint32_t*)(b + off_t);
-    uint32_t* bin_off = bin_hist + (size_t)kBins * kBinBlocks;
-    void* scan_tmp = (char*)(bin_off + (size_t)kBins * kBinBlocks) + 256;
+    uint32_t* bin_rowsum = bin_hist + (size_t)kBins * kBinBlocks;
+    uint32_t* bin_base = bin_rowsum + kBins;
 #endif
     bool sorted = false;   // this step's lists are in lists_o
 #if PT_WF_BIN
     auto bin_sort = [&]() -> hipError_t {   // (the device reads the list's length: no host wait)
         hipLaunchKernelGGL(k_bin_hist, dim3(kBinBlocks), dim3(256), 0, st, (const uint16_t*)keys,
                            (const int32_t*)counters, bin_hist);
-        size_t tb = sz_tmp;
-        const hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, (const uint32_t*)bin_hist, bin_off,
-                                                              kBins * kBinBlocks, st);
-        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_bin_rows, dim3(kBins / 4), dim3(256), 0, st, bin_hist, (const int32_t*)counters,
+                           bin_rowsum);
+        hipLaunchKernelGGL(k_bin_base, dim3(1), dim3(1024), 0, st, (const uint32_t*)bin_rowsum, bin_base);
         hipLaunchKernelGGL(k_bin_scatter, dim3(kBinBlocks), dim3(256), 0, st, (const uint16_t*)keys,
-                           (const int32_t*)lists, (const int32_t*)counters, (const uint32_t*)bin_off, lists_o);
+                           (const int32_t*)lists, (const int32_t*)counters, (const uint32_t*)bin_hist,
+                           (const uint32_t*)bin_base, lists_o);
         sorted = true;
         return hipGetLastError();
     };
@@ -1200,9 +1265,11 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     const bool times = (flags & PT_FLAG_KERNEL_TIMES) != 0 && stats;
     unsigned long long* wc = (unsigned long long*)s->stats;   // [0..2] shadow, [3..5] closest
     if (wcount) HIPCHK(hipMemsetAsync(s->stats, 0, sizeof(StatsDev), st));
-    // per-kernel HIP events (PT_FLAG_KERNEL_TIMES): shade, shadow, closest x (start, end) per step
+    // per-kernel HIP events (PT_FLAG_KERNEL_TIMES): shade, shadow, closest, the
+    // shadow list's sort x (start, end) per step
+    constexpr int kEv = 8;
     if (times) {
-        const size_t ne = (size_t)steps * 6;
+        const size_t ne = (size_t)steps * kEv;
         while (s->prof_ev.size() < ne) {
             hipEvent_t e;
             HIPCHK(hipEventCreate(&e));
@@ -1210,7 +1277,7 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
         }
     }
     auto mark = [&](int32_t step, int k, int end, hipStream_t on) -> hipError_t {
-        return times ? hipEventRecord(s->prof_ev[(size_t)step * 6 + k * 2 + end], on) : hipSuccess;
+        return times ? hipEventRecord(s->prof_ev[(size_t)step * kEv + k * 2 + end], on) : hipSuccess;
     };
     // step 0 walks the primary queries (CQP, one per pixel), later steps the slots' (CQ)
     auto closest_walk = [&](hipStream_t on, int32_t step) {
@@ -1266,7 +1333,11 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
 #if PT_WF_BIN
             // the shadow list sorted by the origin's cell (the device reads
             // its length) while the closest walks, unsorted, already run
-            if (step > 0) HIPCHK(bin_sort());   // (step 0: the primary rays)
+            if (step > 0) {   // (step 0: the primary rays)
+                HIPCHK(mark(step, 3, 0, st));
+                HIPCHK(bin_sort());
+                HIPCHK(mark(step, 3, 1, st));
+            }
 #endif
             HIPCHK(mark(step, 1, 0, st));
             shadow_walk(st);
@@ -1292,19 +1363,21 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
             stats->closest_leaf_units = h.v[5];
         }
         if (times) {
-            double t[3] = {0, 0, 0};
-            uint64_t n[3] = {0, 0, 0};
+            double t[4] = {0, 0, 0, 0};
+            uint64_t n[4] = {0, 0, 0, 0};
             for (int32_t step = 0; step < steps; ++step)
-                for (int k = 0; k < 3; ++k) {
+                for (int k = 0; k < 4; ++k) {
                     if (k > 0 && step + 1 >= steps) continue;
+                    if (k == 3 && (!PT_WF_BIN || step == 0)) continue;
                     float ms = 0.f;
-                    HIPCHK(hipEventElapsedTime(&ms, s->prof_ev[(size_t)step * 6 + k * 2],
-                                               s->prof_ev[(size_t)step * 6 + k * 2 + 1]));
+                    HIPCHK(hipEventElapsedTime(&ms, s->prof_ev[(size_t)step * kEv + k * 2],
+                                               s->prof_ev[(size_t)step * kEv + k * 2 + 1]));
                     t[k] += ms;
                     ++n[k];
                 }
             stats->shade_ms = t[0]; stats->shadow_ms = t[1]; stats->closest_ms = t[2];
             stats->shade_launches = n[0]; stats->shadow_launches = n[1]; stats->closest_launches = n[2];
+            stats->sort_ms = t[3]; stats->sort_launches = n[3];
         }
     }
     return PT_OK;
@@ -1468,8 +1541,9 @@ static void add_stats(pt_stats* d, const pt_stats& s) {
     d->shade_ms += s.shade_ms; d->shadow_ms += s.shadow_ms; d->closest_ms += s.closest_ms;
     d->shade_launches += s.shade_launches; d->shadow_launches += s.shadow_launches;
     d->closest_launches += s.closest_launches;
+    d->sort_ms += s.sort_ms; d->sort_launches += s.sort_launches;
 }
-static_assert(sizeof(pt_stats) == 17 * 8 + 3 * 8, "add_stats covers every pt_stats field");
+static_assert(sizeof(pt_stats) == 19 * 8 + 3 * 8, "add_stats covers every pt_stats field");
 
 extern "C" {
 

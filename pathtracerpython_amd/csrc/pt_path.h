@@ -448,6 +448,52 @@ PT_HD float pt_canon(float x) {
     return x;
 #endif
 }
+// PT_MMERGE: a shadow ray's two member tests of a unit as ONE pair of margins.
+// Both members share the plane part (cm, nm, del), and a shadow ray only asks
+// whether the unit occludes it (both members are one object), so with
+// M = max(m0, m1):
+//   c = min(cm, M - del) > 0   iff some member is a certain occluder
+//                              (c_i = min(cm, m_i - del) > 0 for M's member)
+//   a = min(nm, M + del, -c)   >= 0 whenever some member's test is ambiguous
+//                              and no member occludes for certain
+// (margin_unit; if one member occludes for certain, the other's ambiguity
+// decides nothing: rays 0, 1 are occluded, ray 2's object is this unit's).
+// For rays 0, 1 the "not occluded before this unit" term folds in as
+// -max(old, c), the new occlusion margin.  The rare block rebuilds the
+// per-member bits as before (shadow_bits_m), so the f64 decisions are the
+// same ones; hostcheck's filter self-test checks both claims test by test.
+#ifndef PT_MMERGE
+#define PT_MMERGE 1
+#endif
+PT_HD void margin_unit(float cm, float nm, float M, float del, float* c, float* a) {
+    *c = nan_min(cm, M - del);
+    *a = fminf(fminf(nm, M + del), -*c);
+}
+// fmaxf of two quiet-NaN-or-number values without the canonicalising
+// v_max_f32 x, x the compiler puts before an IEEE-mode v_max_f32 whose input
+// comes through a phi: v_med3_f32(a, b, +inf) is max(a, b), and with a NaN
+// input it returns v_min3_f32(a, b, +inf), i.e. the other operand (fmaxf's
+// result).  The values here come from arithmetic (quiet NaNs only).
+PT_HD float fmax_q(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmaxf(a, b);
+#endif
+}
+// nan_min(nan_min(a, b), c) as one v_minimum3_f32 (the compiler emits each
+// two-input minimum as its own v_minimum3_f32 with a repeated operand)
+PT_HD float nan_min3(float a, float b, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r;
+    asm("v_minimum3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return nan_min(nan_min(a, b), c);
+#endif
+}
 PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool coplanar,
                          ShadowSet* sh, float oc[kLightSamples], uint32_t* amb, float* amax = nullptr) {
     const float cop = PT_MICRO ? pt_canon(coplanar ? -1.0f : INFINITY) : (coplanar ? -1.0f : INFINITY);
@@ -463,6 +509,33 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
         // triangle part only runs when some lane of the wave is not
         // certainly out of range (K2 6.49 -> 6.35 ms).
         if (!PT_WAVE_ANY(!(nm < 0.0f))) continue;
+#if PT_QUAD && PT_MMERGE
+        if (PT_AMB_MAX && amax) {
+            const QuadM m = quad_m(U, p, O, d);
+            const float M = fmax_q(m.m0, m.m1);
+            const float old = oc[k];
+            // c = min(cm, M - del), cm's five terms in two v_minimum3
+            const float c = nan_min3(nan_min3(fabsf(p.q) - U.qhi, (p.at - p.dt) - kTzHi,
+                                              sh->hlo[k] - (p.at + p.dt)),
+                                     cop, M - p.del);
+            if (k == kLightSamples - 1) {
+                const bool need = U.obj < sh->key2;
+                if (c > 0.0f && need) {
+                    sh->key2 = U.obj;
+                    sh->leak = U.obj;
+                }
+                *amax = fmax_q(*amax, need ? fminf(fminf(nm, M + p.del), -c) : -1.0f);
+                oc[k] = fmax_q(old, c);
+            } else {   // only while not occluded before this unit: -max(old, c)
+                const float occ = fmax_q(old, c);
+                const float a = fminf(fminf(nm, M + p.del), -occ);   // (never NaN: nm is not)
+                // ray 0 comes first and *amax enters at -1: only its sign is read
+                *amax = k == 0 ? a : fmax_q(*amax, a);
+                oc[k] = occ;
+            }
+            continue;
+        }
+#endif
 #if PT_QUAD
         const QuadM m = quad_m(U, p, O, d);
         float c0, a0, c1, a1;

@@ -28,6 +28,6 @@ print("fb sha", hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16])
 if "--times" in sys.argv:   # each kernel's own time (the walks one after the other)
     from pathtracerpython_amd._abi import PT_FLAG_KERNEL_TIMES, with_flags
     _, kt = r.render_params(with_flags(p, PT_FLAG_KERNEL_TIMES), stats=True)
-    print("own ms per render: shade %.1f shadow %.1f closest %.1f (launches %d / %d / %d)" % (
-        kt["shade_ms"], kt["shadow_ms"], kt["closest_ms"], kt["shade_launches"], kt["shadow_launches"],
-        kt["closest_launches"]))
+    print("own ms per render: shade %.1f shadow %.1f closest %.1f sort %.1f (launches %d / %d / %d / %d)" % (
+        kt["shade_ms"], kt["shadow_ms"], kt["closest_ms"], kt["sort_ms"], kt["shade_launches"],
+        kt["shadow_launches"], kt["closest_launches"], kt["sort_launches"]))

@@ -325,6 +325,15 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
                 margin_plane(U, ps, hlo, hhi, INFINITY, &cm, &nm);
                 const OriginU Oq = origin_q(U, at_eye ? o32 : o32s);
                 const QuadM qs = quad_m(U, ps, Oq, d32), qc = quad_m(U, pc, Oq, d32);
+                {   // the merged unit margins (PT_MMERGE, margin_unit) against the members'
+                    float c0, a0, c1, a1, cu, au;
+                    margin_m(qs.m0, ps, cm, nm, &c0, &a0);
+                    margin_m(qs.m1, ps, cm, nm, &c1, &a1);
+                    margin_unit(cm, nm, fmaxf(qs.m0, qs.m1), ps.del, &cu, &au);
+                    const bool occ = c0 > 0.0f || c1 > 0.0f;
+                    if ((cu > 0.0f) != occ) ++mdiff;                           // occlusion: same verdict
+                    if (!occ && (a0 >= 0.0f || a1 >= 0.0f) && !(au >= 0.0f)) ++mdiff;   // no lost f64 test
+                }
                 for (int i = 0; i < 2; ++i) {
                     D3 Q; double sqd;
                     const bool h = i < U.count && eval64(H.trid[U.t[i]], o, dn, &Q, &sqd);

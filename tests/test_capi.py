@@ -40,12 +40,12 @@ def test_abi_struct_layout(hostcheck):
                          PtStats.shadow_queries.offset, PtStats.shade_ms.offset,
                          PtStats.closest_launches.offset, PtSceneDesc.light_rgb.offset,
                          PtRenderParams.sample_begin.offset]
-    assert C.sizeof(PtStats) == 14 * 8 + 3 * 8 + 3 * 8
+    assert C.sizeof(PtStats) == 14 * 8 + 3 * 8 + 3 * 8 + 2 * 8
 
 
 def test_api_version():
     from pathtracerpython_amd._abi import PT_API_VERSION
-    assert _native.lib().pt_api_version() == PT_API_VERSION == 6
+    assert _native.lib().pt_api_version() == PT_API_VERSION == 7
 
 
 @pytest.mark.parametrize("H,step,phase,b,e", [(10, 1, 0, 0, 10), (10, 3, 1, 0, 10),

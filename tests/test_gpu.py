@@ -550,6 +550,8 @@ def test_wavefront_walk_counts_and_times(k5small):
         assert np.array_equal(fb, ref)
         assert tt["shade_launches"] == tt["shadow_launches"] + 1 == tt["closest_launches"] + 1
         assert tt["shade_ms"] > 0 and tt["shadow_ms"] > 0 and tt["closest_ms"] > 0
+        # (C-ABI v7) the shadow list's sort, its own interval: every walk step but the first
+        assert tt["sort_launches"] == tt["shadow_launches"] - 1 and tt["sort_ms"] > 0
 
 
 def test_render_multi_lanes_contract(cornell):
