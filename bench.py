@@ -166,6 +166,38 @@ def load_traffic(config):
     return d.get("hbm_bytes_per_launch"), d.get("source")
 
 
+def device_identity():
+    """This rank's GPU as the driver can check it: the torch device index and
+    the PCI location (domain:bus:device) and UUID of that device."""
+    import torch
+    dev = torch.cuda.current_device()
+    pr = torch.cuda.get_device_properties(dev)
+    return {"local_device": dev,
+            "pci_bus_id": "%04x:%02x:%02x" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id),
+            "uuid": str(getattr(pr, "uuid", ""))}
+
+
+def rank_records(me, dist, world):
+    """Every rank's record (rank order), on every rank (control group: gloo)."""
+    if world == 1:
+        return [me]
+    out = [None] * world
+    dist.all_gather_object(out, me)
+    return out
+
+
+def duplicate_devices(ranks):
+    """PCI bus ids that more than one rank reports (a rank-to-device mistake:
+    N ranks on fewer than N GPUs would still print a plausible line)."""
+    seen, dup = set(), []
+    for r in ranks:
+        b = r["pci_bus_id"]
+        if b in seen and b not in dup:
+            dup.append(b)
+        seen.add(b)
+    return dup
+
+
 def rank_legs(vals, dist, world):
     """(max, min) over ranks of this rank's value (control group: gloo)."""
     if world == 1:
@@ -410,6 +442,8 @@ def run_device_frame(ctx, steps, warmup):
     elapsed = time.perf_counter() - t0
     legs = {k: [e[j].elapsed_time(e[j + 1]) for e in evs]
             for j, k in enumerate(("render", "gather", "assembly", "d2h"))}
+    # the gather's communicator as RCCL reports it (1: no gather at N = 1)
+    legs["rccl_world"] = dist.get_world_size(group) if group is not None else 1
     if group is not None:
         dist.destroy_process_group(group)
     return elapsed, legs, (host.numpy().copy() if rank == 0 else None)
@@ -432,6 +466,11 @@ def main():
     # timings mean nothing: the ranks share the GPU)
     rehearse = os.environ.get("PT_BENCH_REHEARSE") == "1"
     if rehearse:
+        local = 0
+        args.frame = "host"
+    elif os.environ.get("PT_BENCH_FORCE_DEVICE0") == "1":
+        # (tests only) the rank-to-device mistake on purpose, without the
+        # rehearsal's licence: the job must refuse to print a line
         local = 0
         args.frame = "host"
     torch.cuda.set_device(local)
@@ -529,11 +568,26 @@ def main():
             for k in ("gather", "assembly", "d2h"):
                 lg[k] = round(float(np.mean(legs[k])), 4)
         return {"ms_per_step": round(ms, 4), "value": round(paths / (ms * 1e-3) / 1e6, 2),
-                "legs_ms": lg, "_k_ms": km, "_fb": fb}
+                "legs_ms": lg, "rccl_world": legs["rccl_world"], "_k_ms": km, "_fb": fb}
 
     # 1. the headline transport
     head = host_mode(0) if args.frame == "host" else device_mode()
     other_name = "device" if args.frame == "host" else "host"
+    # which GPU every rank ran on, with its own band kernel time: the line
+    # certifies that N ranks used N distinct GPUs; two ranks
+    # on one device end the job without a line, except in the one-GPU
+    # rehearsal (PT_BENCH_REHEARSE), where the ranks share device 0 on purpose
+    ranks = rank_records(dict(rank=rank, **device_identity(), band_kernel_ms=round(head["_k_ms"], 4)),
+                         dist, world)
+    dup = duplicate_devices(ranks)
+    if dup and not rehearse:
+        print(f"bench: ranks share a GPU ({', '.join(dup)}): {ranks}; no line printed "
+              "(one rank per GPU is the contract)", file=sys.stderr, flush=True)
+        if hf is not None:
+            hf.discard()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(3)
     k_ms = head["_k_ms"]
     fb = head["_fb"]
     ms_per_step = head["ms_per_step"]
@@ -622,6 +676,8 @@ def main():
                                       "RCCL gather + device assembly (N > 1) + D2H copy")},
             "frame_modes": {args.frame: {k: v for k, v in head.items() if not k.startswith("_")},
                             other_name: {"pending": "runs after the headline"}},
+            "ranks": ranks,
+            "ranks_share_a_gpu": dup or None,
             "host_frame_error": hf_err,
             "linf_vs_cpu_ref": linf, "linf_checked": checked, "pixels_over": over,
             "roofline": roofline,

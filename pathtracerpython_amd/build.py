@@ -62,11 +62,22 @@ def _stale(out=OUT, csrc=CSRC):
     return embedded_build_id(out) != source_sha(csrc)
 
 
+def variant_id(sha, defines):
+    """The id of a build with -D switches: the sources' hash folded with the
+    sorted switches, so a variant never carries the default build's id — it
+    loads only with PT_ALLOW_FOREIGN_BUILD=1 and is always named by its own id
+    (ADVICE r05)."""
+    if not defines:
+        return sha
+    h = hashlib.sha256((sha + "\0" + "\0".join(sorted(defines))).encode())
+    return h.hexdigest()[:ID_LEN]
+
+
 def compile_lib(out, defines=(), csrc=CSRC, verbose=True):
     """hipcc the library into `out`, stamped with the hash of `csrc`'s sources
-    (dev variants pass -D switches; they carry the same id when built from the
-    same sources)."""
-    sha = source_sha(csrc)
+    (dev variants pass -D switches: their id also covers the switches,
+    variant_id)."""
+    sha = variant_id(source_sha(csrc), tuple(defines))
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ([HIPCC] + FLAGS + [f"-DPT_BUILD_ID=\"{sha}\""] + ["-D" + d for d in defines] +
            ["-o", out + ".tmp"] +

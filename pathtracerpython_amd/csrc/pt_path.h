@@ -13,6 +13,7 @@
 // origin terms of each test are computed once.
 #pragma once
 #include "pt_core.h"
+#include <assert.h>
 
 #if defined(__HIP_DEVICE_COMPILE__)
 #define PT_WAVE_ALL(x) (__all(x) != 0)
@@ -306,6 +307,9 @@ PT_HD D3 light_redraw(const SceneK& S, uint64_t seed, uint32_t pixel, uint32_t s
 // the sample index and the bounce are the record's si and sb, just below
 // the home (offsets checked in pt_wavefront.h).  sp: a wavefront home only.
 PT_HD D3 wf_light(const SceneK& S, const Spill& sp, int k) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    assert(sp.stride == 1 && "wf_light: a wavefront path record's home (stride 1) only");
+#endif
     const double* base = sp.base;
     uint64_t w0, w1, w2;
     const double d0 = sp.get(kSpL), d1 = sp.get(kSpL + 1), d2 = sp.get(kSpL + 2);
@@ -396,7 +400,7 @@ PT_HD QuadM quad_m(const UnitF& U, const RayPlane& p, const OriginU& O, F3 d) {
     return r;
 }
 #ifndef PT_MICRO
-#define PT_MICRO 2
+#define PT_MICRO 6
 #endif
 // origin terms of the render loop's unit form (the second member's only for
 // a pair that is no parallelogram), and (PT_VCONST) VGPR copies of the
@@ -414,7 +418,14 @@ PT_HD OriginU origin_q(const UnitF& U, F3 o) {
     r.h = aff3(U.n, U.cn, o);
     r.bo0 = aff3(U.tri[0].gb, U.tri[0].cb, o);
     r.co0 = aff3(U.tri[0].gc, U.tri[0].cc, o);
+#if PT_MICRO >= 6 && defined(__HIP_DEVICE_COMPILE__)
+    // (6) bo1 / co1 are read only under U.quad < 0 (quad_m), where they are
+    // set: no zero default (two v_mov per unit for the phi)
+    r.bo1 = r.bo0;   // (any value: unread unless overwritten below)
+    r.co1 = r.co0;
+#else
     r.bo1 = r.co1 = 0.f;
+#endif
     if (U.quad < 0) {   // wave-uniform
 #if PT_MICRO >= 2 && defined(__HIP_DEVICE_COMPILE__)
         // (3) an opaque copy of the origin: the compiler otherwise computes
@@ -465,6 +476,12 @@ PT_HD float pt_canon(float x) {
 #ifndef PT_MMERGE
 #define PT_MMERGE 1
 #endif
+#ifndef PT_CLOSEST_LEAN
+#define PT_CLOSEST_LEAN 1
+#endif
+#ifndef PT_DEL_PRE
+#define PT_DEL_PRE 0
+#endif
 PT_HD void margin_unit(float cm, float nm, float M, float del, float* c, float* a) {
     *c = nan_min(cm, M - del);
     *a = fminf(fminf(nm, M + del), -*c);
@@ -475,7 +492,9 @@ PT_HD void margin_unit(float cm, float nm, float M, float del, float* c, float* 
 // input it returns v_min3_f32(a, b, +inf), i.e. the other operand (fmaxf's
 // result).  The values here come from arithmetic (quiet NaNs only).
 PT_HD float fmax_q(float a, float b) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && PT_FMAX_MED3
+    return __builtin_amdgcn_fmed3f(a, b, 3.40282347e38f);
+#elif defined(__HIP_DEVICE_COMPILE__)
     float r;
     asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
@@ -500,7 +519,12 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
 #pragma unroll
     for (int k = 0; k < kLightSamples; ++k) {
         const F3 d = sh->d32[k];
+#if PT_DEL_PRE && defined(__HIP_DEVICE_COMPILE__)
+        const RayPlane p0 = ray_plane_e(U, O.h, d, sh->hlo[k], sh->hhi[k], O.eh, O.eo);
+        const RayPlane& p = p0;
+#else
         const RayPlane p = ray_plane_e(U, O.h, d, sh->hlo[k], sh->hhi[k], O.eh, O.eo);
+#endif
         float cm, nm;
         margin_plane(U, p, sh->hlo[k], sh->hhi[k], cop, &cm, &nm);
         // nm < 0 (the plane part is a certain miss; nm is never NaN, cop is
@@ -508,9 +532,26 @@ PT_HD void shadow_unit_m(const SceneK& S, const UnitF& U, const OriginU& O, bool
         // negative or a dropped NaN: no occlusion, no ambiguous test.  The
         // triangle part only runs when some lane of the wave is not
         // certainly out of range (K2 6.49 -> 6.35 ms).
+#if PT_QUAD && PT_MMERGE && PT_MICRO >= 5
+        // (5) ray 0 comes first and *amax enters at -1, only its sign is
+        // read: when the wave skips the ray every lane's nm is < 0 (never
+        // NaN), so nm serves as the "nothing ambiguous" value — no -1.0
+        // constant materialised for the skip edge
+        if (k == 0 && PT_AMB_MAX && amax) *amax = nm;
+#endif
+#if PT_DEL_PRE && defined(__HIP_DEVICE_COMPILE__)
+        // (dev) del's |t| ed + eo term before the vote, where |t| is a source
+        // modifier (after the branch the compiler materialises |t| with a v_and)
+        float ye = fmaf(p.at, U.ed, O.eo);
+        asm("" : "+v"(ye));
+#endif
         if (!PT_WAVE_ANY(!(nm < 0.0f))) continue;
 #if PT_QUAD && PT_MMERGE
         if (PT_AMB_MAX && amax) {
+#if PT_DEL_PRE && defined(__HIP_DEVICE_COMPILE__)
+            RayPlane p = p0;
+            p.del = fmaf(U.g, p.dt, ye);
+#endif
             const QuadM m = quad_m(U, p, O, d);
             const float M = fmax_q(m.m0, m.m1);
             const float old = oc[k];
@@ -709,8 +750,20 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
         }
     }
     if (!FORCE64 && do_closest && (rays & 8u)) {
-        const RayPlane p = (MARGIN && PT_QUAD) ? ray_plane_e(U, O.h, n32, INFINITY, INFINITY, O.eh, O.eo)
-                                               : ray_plane(U, O.h, n32, INFINITY, INFINITY);
+        RayPlane p = (MARGIN && PT_QUAD) ? ray_plane_e(U, O.h, n32, INFINITY, INFINITY, O.eh, O.eo)
+                                         : ray_plane(U, O.h, n32, INFINITY, INFINITY);
+#if PT_CLOSEST_LEAN
+        if (MARGIN && PT_QUAD) {
+            // the closest ray's range has no far end (hi_lo = hi_hi = inf):
+            // rcand's "at + dt < inf" follows from |q| > qhi (>= 1e-5: |t| <=
+            // |h| 1e5 (1 + u), dt finite, for the finite origins and records
+            // here), and rmiss's "at - dt >= inf" only holds for |t| = inf (q
+            // exactly 0), which is then ambiguous (del = inf) and decided in
+            // f64 — two compares less per unit, the same certain verdicts
+            p.rcand = (fabsf(p.q) > U.qhi) & (p.at - p.dt > kTzHi);
+            p.rmiss = p.at + p.dt < kTzLo;
+        }
+#endif
         bool c0, a0, c1 = false, a1 = false;
         if (MARGIN && PT_QUAD) {   // the render loop's unit form (quad_m)
             const QuadM m = quad_m(U, p, O, n32);
@@ -1491,11 +1544,15 @@ PT_HD bool shadow1_open(const SceneK& S, const Shadow1& r) {
 }
 // the f64 decisions of a unit's ambiguous tests for the ray (a0, a1)
 // (inline: an out-of-line call's frame made the walk 2x slower)
+// LRNG: the spill home is a wavefront path record's (stride 1) whose light
+// points are not kept (PT_WF_LRNG): draw the point again from its RNG key
+// (wf_light).  Every caller says which home it passes.
+template <bool LRNG>
 PT_HD void shadow1_fallback(const SceneK& S, const UnitF& U, bool a0, bool a1, Shadow1* r,
                       const Spill& sp) {
     const bool last = r->k == kLightSamples - 1;
     const D3 P = sp.get3(kSpP);
-    const D3 L = PT_WF_LRNG ? wf_light(S, sp, r->k) : sp.get3(kSpL + 3 * r->k);   // (the walks' only)
+    const D3 L = LRNG ? wf_light(S, sp, r->k) : sp.get3(kSpL + 3 * r->k);
     for (int i = 0; i < 2; ++i) {
         if (!(i == 0 ? a0 : a1)) continue;
         if (last ? (U.obj >= r->key2) : r->occ) continue;   // decided meanwhile
@@ -1513,6 +1570,7 @@ PT_HD void shadow1_fallback(const SceneK& S, const UnitF& U, bool a0, bool a1, S
 }
 // one BVH unit against the ray (fused_unit's shadow part for one ray, its
 // f64 fallback included: same verdicts, same decisions)
+template <bool LRNG>
 PT_HD void shadow1_unit(const SceneK& S, const UnitF& U, F3 o32, int ogrp, Shadow1* r,
                         const Spill& sp) {
     const OriginU O = origin_u(U, o32);
@@ -1536,7 +1594,7 @@ PT_HD void shadow1_unit(const SceneK& S, const UnitF& U, F3 o32, int ogrp, Shado
             r->leak = U.obj;
         }
     }
-    if (need && (a0 | a1)) shadow1_fallback(S, U, a0, a1, r, sp);
+    if (need && (a0 | a1)) shadow1_fallback<LRNG>(S, U, a0, a1, r, sp);
 }
 struct ShadowTrav1 {
     F3 o32, inv;
@@ -1599,11 +1657,11 @@ PT_HD void s1_qnode(ShadowTrav1& T, const KS& K, const SceneK& S, const Shadow1&
     T.ref = d[0] < INFINITY ? rf[0] : s1_pop(T, K, S, r);
 }
 // the units of leaf `ref` (<= -2)
-template <bool UC>
+template <bool UC, bool LRNG>
 PT_HD void s1_units(const ShadowTrav1& T, const SceneK& S, Shadow1* r, const Spill& sp, int ref) {
     const int code = ~ref, u0 = code >> 3, nu = code & 7;
     for (int i = 0; i < nu && shadow1_open(S, *r); ++i)
-        shadow1_unit(S, bvh_unit<UC>(S, u0 + i), T.o32, T.ogrp, r, sp);
+        shadow1_unit<LRNG>(S, bvh_unit<UC>(S, u0 + i), T.o32, T.ogrp, r, sp);
 }
 
 // Standalone query (primary rays, the batched intersect_objects API).  d need

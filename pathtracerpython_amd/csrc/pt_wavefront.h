@@ -244,6 +244,10 @@ PT_HD uint32_t wf_begin_bounce(const SceneK& S, const LaneJob& J, WfPath* W, WfS
     sh.leak = S.n_obj - 1;
     rng_block(J.seed, J.pixel, sample, (uint32_t)b, 3u, &w[12]);
 #else
+    // (shadow_setup stores the light points into the home's kSpL slots, where
+    // a PT_WF_LRNG record keeps its RNG key: the two switches exclude each
+    // other)
+    static_assert(!PT_WF_LRNG, "PT_WF_LRNG needs PT_RNG_PERBLOCK (the light points must not overwrite the key)");
     rng_blocks4(J.seed, J.pixel, sample, (uint32_t)b, w);
     {
         double u12[12];

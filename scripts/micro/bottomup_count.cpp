@@ -95,8 +95,8 @@ void drain(const Tree4& T, const SceneK& S, ShadowTrav1& tv, Shadow1& r, const S
         }
         if (x != kNoRef) {
             c->units += (~x) & 7;
-            if (S.bunitc) s1_units<true>(tv, S, &r, sp, x);
-            else s1_units<false>(tv, S, &r, sp, x);
+            if (S.bunitc) s1_units<true, PT_WF_LRNG != 0>(tv, S, &r, sp, x);
+            else s1_units<false, PT_WF_LRNG != 0>(tv, S, &r, sp, x);
         }
     }
 }
@@ -129,8 +129,8 @@ void shadow_bottomup(const Tree4& T, const SceneK& S, int u, F3 o32, int ogrp, S
     if (shadow1_open(S, r)) {
         const int32_t leaf = ~((u << 3) | 1);
         c->units += 1;
-        if (S.bunitc) s1_units<true>(tv, S, &r, sp, leaf);
-        else s1_units<false>(tv, S, &r, sp, leaf);
+        if (S.bunitc) s1_units<true, PT_WF_LRNG != 0>(tv, S, &r, sp, leaf);
+        else s1_units<false, PT_WF_LRNG != 0>(tv, S, &r, sp, leaf);
     }
     int32_t cur = T.leaf_parent[u], from = T.leaf_slot[u];
     while (cur >= 0 && shadow1_open(S, r)) {
@@ -218,8 +218,8 @@ int bu_count(const pt_scene_desc* d, const pt_render_params* p, int64_t* out) {
                 while (T1.ref != kNoRef) {
                     while (T1.ref >= 0) s1_qnode(T1, K, H.k, r);
                     if (T1.ref != kNoRef) {
-                        if (H.k.bunitc) s1_units<true>(T1, H.k, &r, sp, T1.ref);
-                        else s1_units<false>(T1, H.k, &r, sp, T1.ref);
+                        if (H.k.bunitc) s1_units<true, PT_WF_LRNG != 0>(T1, H.k, &r, sp, T1.ref);
+                        else s1_units<false, PT_WF_LRNG != 0>(T1, H.k, &r, sp, T1.ref);
                         T1.ref = s1_pop(T1, K, H.k, r);
                     }
                 }

@@ -215,8 +215,8 @@ void shadow_wide(const WTree& T, const SceneK& S, F3 o32, int ogrp, Shadow1 r, c
         if (x != kNoRef) {
             ++c->leaves;
             c->units += (~x) & 7;
-            if (S.bunitc) s1_units<true>(tv, S, &r, sp, x);
-            else s1_units<false>(tv, S, &r, sp, x);
+            if (S.bunitc) s1_units<true, PT_WF_LRNG != 0>(tv, S, &r, sp, x);
+            else s1_units<false, PT_WF_LRNG != 0>(tv, S, &r, sp, x);
         }
     }
     if (r.occ != expect.occ || r.key2 != expect.key2 || r.leak != expect.leak) ++c->mismatches;
@@ -344,8 +344,8 @@ int wx_count(const pt_scene_desc* d, const pt_render_params* p, int64_t* out, in
                         ++g_hint[1];
                         Shadow1 rh = r0;
                         tv_dummy.o32 = o32; tv_dummy.ogrp = ogrp;
-                        if (H.k.bunitc) shadow1_unit(H.k, bvh_unit<true>(H.k, hu), o32, ogrp, &rh, sp);
-                        else shadow1_unit(H.k, bvh_unit<false>(H.k, hu), o32, ogrp, &rh, sp);
+                        if (H.k.bunitc) shadow1_unit<PT_WF_LRNG != 0>(H.k, bvh_unit<true>(H.k, hu), o32, ogrp, &rh, sp);
+                        else shadow1_unit<PT_WF_LRNG != 0>(H.k, bvh_unit<false>(H.k, hu), o32, ogrp, &rh, sp);
                         if (!shadow1_open(H.k, rh)) g_hint_hit_pending = true;
                     }
                 }
@@ -357,8 +357,8 @@ int wx_count(const pt_scene_desc* d, const pt_render_params* p, int64_t* out, in
                         ++ws[2];
                         ws[3] += (~T.ref) & 7;
                         const bool was_open = shadow1_open(H.k, r);
-                        if (H.k.bunitc) s1_units<true>(T, H.k, &r, sp, T.ref);
-                        else s1_units<false>(T, H.k, &r, sp, T.ref);
+                        if (H.k.bunitc) s1_units<true, PT_WF_LRNG != 0>(T, H.k, &r, sp, T.ref);
+                        else s1_units<false, PT_WF_LRNG != 0>(T, H.k, &r, sp, T.ref);
                         if (was_open && !shadow1_open(H.k, r)) closer = ~T.ref >> 3;
                         T.ref = s1_pop(T, K, H.k, r);
                     }

@@ -3,7 +3,7 @@
 # prof_k5.py).  Usage: bash scripts/pmc_wf.sh TAG [lib.so] -> gpurun_out/pmc_wf_TAG/{shade,shadow,closest}.json
 set -euo pipefail
 R=$PWD; TAG=${1:-base}; OUT=$R/gpurun_out/pmc_wf_$TAG; mkdir -p $OUT
-if [ -n "${2:-}" ]; then export PT_HIP_LIB=$(readlink -f "$2"); fi
+if [ -n "${2:-}" ]; then export PT_HIP_LIB=$(readlink -f "$2") PT_ALLOW_FOREIGN_BUILD=1; fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES --output-format csv -d $OUT/p1 -o p -- python3 $R/scripts/prof_k5.py 1 512 64 > $OUT/p1.log 2>&1
 timeout -k 10 200 rocprofv3 --kernel-trace --pmc SQ_THREAD_CYCLES_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/p2 -o p -- python3 $R/scripts/prof_k5.py 1 512 64 > $OUT/p2.log 2>&1

@@ -10,6 +10,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gp
 for v in "$R"/pathtracerpython_amd/_lib/variants/*.so; do
     [ -e "$v" ] || continue
     n=$(basename "$v" .so)
-    PT_HIP_LIB="$v" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+    PT_ALLOW_FOREIGN_BUILD=1 PT_HIP_LIB="$v" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$R/gpurun_out/pc_$n" -o k5 -- python3 "$R/scripts/prof_k5.py" 2 512 64 > "$R/gpurun_out/pc_$n.log" 2>&1
 done

@@ -13,6 +13,6 @@ for round in $(seq 1 "${ROUNDS:-2}"); do
     for v in "$R"/pathtracerpython_amd/_lib/variants/"$prefix"*.so; do
         [ -e "$v" ] || continue
         echo "== $(basename "$v")"
-        PT_HIP_LIB="$v" timeout -k 10 "${LIMIT:-300}" "$@"
+        PT_ALLOW_FOREIGN_BUILD=1 PT_HIP_LIB="$v" timeout -k 10 "${LIMIT:-300}" "$@"
     done
 done

@@ -11,6 +11,6 @@ for round in $(seq 1 "${ROUNDS:-2}"); do
     for v in "$R"/pathtracerpython_amd/_lib/variants/*.so; do
         [ -e "$v" ] || continue
         echo "== $(basename "$v")"
-        PT_HIP_LIB="$v" timeout -k 10 120 python3 "$R/scripts/prof_k2.py" 20
+        PT_ALLOW_FOREIGN_BUILD=1 PT_HIP_LIB="$v" timeout -k 10 120 python3 "$R/scripts/prof_k2.py" 20
     done
 done

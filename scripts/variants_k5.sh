@@ -8,6 +8,6 @@ timeout -k 10 200 python3 "$R/scripts/k5_parity.py"
 for v in "$R"/pathtracerpython_amd/_lib/variants/*.so; do
     [ -e "$v" ] || continue
     echo "== $(basename "$v")"
-    PT_HIP_LIB="$v" timeout -k 10 200 python3 "$R/scripts/prof_k5.py" 3 512 64
-    PT_HIP_LIB="$v" timeout -k 10 200 python3 "$R/scripts/k5_parity.py"
+    PT_ALLOW_FOREIGN_BUILD=1 PT_HIP_LIB="$v" timeout -k 10 200 python3 "$R/scripts/prof_k5.py" 3 512 64
+    PT_ALLOW_FOREIGN_BUILD=1 PT_HIP_LIB="$v" timeout -k 10 200 python3 "$R/scripts/k5_parity.py"
 done

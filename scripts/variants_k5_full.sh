@@ -6,5 +6,5 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 echo "== main"; timeout -k 10 300 python3 "$R/scripts/prof_k5.py" 2 1024 256
 for v in "$R"/pathtracerpython_amd/_lib/variants/*.so; do
     echo "== $(basename "$v")"
-    PT_HIP_LIB="$v" timeout -k 10 300 python3 "$R/scripts/prof_k5.py" 2 1024 256
+    PT_ALLOW_FOREIGN_BUILD=1 PT_HIP_LIB="$v" timeout -k 10 300 python3 "$R/scripts/prof_k5.py" 2 1024 256
 done

@@ -186,8 +186,8 @@ int hc_render_wavefront2(const pt_scene_desc* d, const pt_render_params* p, doub
                     if (T.ref != kNoRef) {
                         ++ws[2];
                         ws[3] += (~T.ref) & 7;
-                        if (H.k.bunitc) s1_units<true>(T, H.k, &r, sp, T.ref);
-                        else s1_units<false>(T, H.k, &r, sp, T.ref);
+                        if (H.k.bunitc) s1_units<true, PT_WF_LRNG != 0>(T, H.k, &r, sp, T.ref);
+                        else s1_units<false, PT_WF_LRNG != 0>(T, H.k, &r, sp, T.ref);
                         T.ref = s1_pop(T, K, H.k, r);
                     }
                 }
@@ -349,6 +349,14 @@ int hc_filter_selftest(const pt_scene_desc* d, int64_t n_rays, uint64_t seed, in
                     ++tests;
                     if (vc == kAmb) ++amb;
                     else if ((vc == kCand) != ref_c) ++wrong;
+                    {   // the render loop's lean closest range (PT_CLOSEST_LEAN): no wrong certain verdict
+                        RayPlane pl = pc;
+                        pl.rcand = (fabsf(pl.q) > U.qhi) & (pl.at - pl.dt > kTzHi);
+                        pl.rmiss = pl.at + pl.dt < kTzLo;
+                        const int vl = verdict_code(verdict_m(i ? qc.m1 : qc.m0, pl));
+                        if (vl != kAmb && (vl == kCand) != ref_c) ++wrong;
+                        if (vl != vc && !(vc == kMiss && vl == kAmb)) ++mdiff;
+                    }
                 }
             }
         }

@@ -77,3 +77,12 @@ def test_line_printed_once_on_a_single_rank():
     res, lines, _ = run(1, inject="raise:0")
     assert res.returncode == 0 and len(lines) == 1
     assert "rank 0: RuntimeError" in lines[0]["frame_modes"]["device"]["error"]
+
+
+def test_duplicate_devices():
+    """bench.py refuses a line when two ranks report one PCI bus id
+    (VERDICT r05 #3); distinct ids pass."""
+    import bench
+    rk = [{"rank": r, "pci_bus_id": "0000:%02x:00" % b} for r, b in enumerate((0x05, 0x15, 0x05, 0x25, 0x15))]
+    assert bench.duplicate_devices(rk) == ["0000:05:00", "0000:15:00"]
+    assert bench.duplicate_devices(rk[:2]) == [] and bench.duplicate_devices(rk[:1]) == []

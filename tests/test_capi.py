@@ -212,3 +212,16 @@ def test_build_is_stale_when_a_source_changes(tmp_path):
         f.write("\n// edit\n")
     assert build.source_sha(str(csrc)) != build.source_sha()
     assert build._stale(csrc=str(csrc))
+
+
+def test_variant_builds_carry_their_own_id():
+    """a build with -D switches is named by the sources AND its
+    switches, so it never passes for the default build (the binding loads it
+    only with PT_ALLOW_FOREIGN_BUILD=1)."""
+    from pathtracerpython_amd import build
+    sha = build.source_sha()
+    assert build.variant_id(sha, ()) == sha
+    v = build.variant_id(sha, ("PT_MMERGE=0",))
+    assert v != sha and len(v) == 16
+    assert build.variant_id(sha, ("A=1", "B=2")) == build.variant_id(sha, ("B=2", "A=1"))
+    assert build.variant_id(sha, ("A=1",)) != build.variant_id(sha, ("A=2",))

@@ -697,6 +697,45 @@ def test_bench_host_frame_path_two_ranks(tmp_path):
     assert line["linf_checked"] == "all 262144 pixels" and line["pixels_over"]["1e-6"] == 0
     legs = line["frame_modes"]["host"]["legs_ms"]
     assert legs["band_kernel_max"] >= legs["band_kernel_min"] > 0
+    # which GPU each rank ran on — here both on device 0, which
+    # only the rehearsal lets through (ranks_share_a_gpu names the bus id)
+    rk = line["ranks"]
+    assert [r["rank"] for r in rk] == [0, 1] and all(r["local_device"] == 0 for r in rk)
+    assert rk[0]["pci_bus_id"] == rk[1]["pci_bus_id"] and len(rk[0]["pci_bus_id"]) == 10
+    assert line["ranks_share_a_gpu"] == [rk[0]["pci_bus_id"]]
+    assert all(r["band_kernel_ms"] > 0 for r in rk)
+    assert max(r["band_kernel_ms"] for r in rk) == pytest.approx(legs["band_kernel_max"], abs=2e-4)
+
+
+def test_bench_refuses_ranks_sharing_a_gpu():
+    """Two ranks on one device without PT_BENCH_REHEARSE (PT_BENCH_FORCE_DEVICE0,
+    the rank-to-device mistake made on purpose): no line, nonzero status."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, PT_BENCH_FORCE_DEVICE0="1")
+    env.pop("PT_BENCH_REHEARSE", None)
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                          "--warmup", "1", "--no-cpu-baseline", "--no-check", "--no-secondary"], env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert res.returncode != 0
+    assert not [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert "ranks share a GPU" in res.stderr
+
+
+def test_bench_line_names_its_gpu():
+    """The N = 1 line: one rank record, and the device-frame leg's RCCL world
+    (1: no gather)."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+                          "--no-cpu-baseline", "--no-check"], capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    line = json.loads([ln for ln in res.stdout.splitlines() if ln.startswith("{")][-1])
+    assert len(line["ranks"]) == 1 and line["ranks"][0]["rank"] == 0 and line["ranks_share_a_gpu"] is None
+    assert line["frame_modes"]["device"]["rccl_world"] == 1
 
 
 @pytest.mark.parametrize("inject", ["raise:1", "hang:1"])
