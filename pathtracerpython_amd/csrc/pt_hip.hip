@@ -26,9 +26,6 @@
 // then walk from nearby origins toward the light, and the shadow walks run
 // 10% faster.  The closest list stays unsorted
 // (random directions: its walks did not gain).
-#ifndef PT_WF_CBIN   // (dev experiment: the closest list sorted by the same origin-cell key)
-#define PT_WF_CBIN 0
-#endif
 #ifndef PT_WF_BIN
 #define PT_WF_BIN 1
 #endif
@@ -342,8 +339,7 @@ constexpr int kShadeBlock = PT_SHADE_BLOCK;
 static_assert(kShadeBlock % 64 == 0 && kShadeBlock >= 128 && kShadeBlock <= 1024, "whole waves, >= 2");
 __device__ __forceinline__ void wf_append_block(uint32_t want, int32_t* counters, int32_t* shadow_list,
                                                 int32_t* closest_list, int32_t slot,
-                                                uint16_t* skeys = nullptr, uint32_t skey = 0,
-                                                uint16_t* ckeys = nullptr) {
+                                                uint16_t* skeys = nullptr, uint32_t skey = 0) {
     constexpr int kWaves = kShadeBlock / 64;
     __shared__ int32_t cnt[2][kWaves], base[2];
     uint64_t m[kLightSamples];
@@ -381,11 +377,7 @@ __device__ __forceinline__ void wf_append_block(uint32_t want, int32_t* counters
             if (skeys) skeys[bs] = (uint16_t)skey;
             shadow_list[bs++] = wf_shadow_entry(slot, k);
         }
-    if (want & kWfWantClosest) {
-        const int32_t pc = bc + (int32_t)lanes_below(mc);
-        closest_list[pc] = slot;
-        if (PT_WF_CBIN && ckeys) ckeys[pc] = (uint16_t)skey;   // (dev experiment)
-    }
+    if (want & kWfWantClosest) closest_list[bc + (int32_t)lanes_below(mc)] = slot;
 }
 // PT_WF_BIN: the shadow list's counting sort on the 12-bit cell key without
 // the host: the list's length n is read on the device.  nb = bin_cols(n)
@@ -543,8 +535,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_wf_shade(SceneK S, RenderK R, i
                                                   WfPath* __restrict__ W, WfShadowQ* __restrict__ SQ,
                                                   WfClosestQ* __restrict__ CQ, const WfClosestQ* __restrict__ CQP,
                                                   int32_t* __restrict__ lists, int32_t* counters,
-                                                  uint32_t slots, uint16_t* __restrict__ keys,
-                                                  uint16_t* __restrict__ ckeys) {
+                                                  uint32_t slots, uint16_t* __restrict__ keys) {
     const uint32_t tid = blockIdx.x * (uint32_t)kShadeBlock + threadIdx.x;
     uint32_t want = 0;
 #if PT_WF_BIN
@@ -568,7 +559,7 @@ __global__ __launch_bounds__(kShadeBlock) void k_wf_shade(SceneK S, RenderK R, i
 #endif
     }
 #if PT_WF_BIN
-    wf_append_block(want, counters, lists, lists + 3 * (size_t)slots, (int32_t)tid, keys, skey, ckeys);
+    wf_append_block(want, counters, lists, lists + 3 * (size_t)slots, (int32_t)tid, keys, skey);
 #elif PT_WF_BLOCK_APPEND
     wf_append_block(want, counters, lists, lists + 3 * (size_t)slots, (int32_t)tid);
 #else
@@ -1223,11 +1214,7 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
                  sz_lo = PT_WF_BIN ? 3 * slots * sizeof(int32_t) : 0;
     const size_t off_k = (off_p + sz_p + 255) / 256 * 256, off_lo = (off_k + sz_k + 255) / 256 * 256,
                  off_t = (off_lo + sz_lo + 255) / 256 * 256;
-    // PT_WF_CBIN (dev): the closest list's keys, its sorted copy and its own sort scratch
-    const size_t sz_ck = PT_WF_CBIN ? slots * sizeof(uint16_t) : 0, sz_clo = PT_WF_CBIN ? slots * sizeof(int32_t) : 0;
-    const size_t off_ck = (off_t + sz_tmp + 255) / 256 * 256, off_clo = (off_ck + sz_ck + 255) / 256 * 256,
-                 off_ct = (off_clo + sz_clo + 255) / 256 * 256;
-    const size_t need = off_ct + (PT_WF_CBIN ? sz_tmp : 0) + 256;
+    const size_t need = off_t + sz_tmp + 256;
     if (need > s->wf_bytes) {
         if (s->wf) (void)hipFree(s->wf);
         s->wf = nullptr;
@@ -1257,10 +1244,6 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
     uint32_t* bin_rowsum = bin_hist + (size_t)kBins * kBinBlocks;
     uint32_t* bin_base = bin_rowsum + kBins;
 #endif
-    uint16_t* ckeys = PT_WF_CBIN ? (uint16_t*)(b + off_ck) : nullptr;
-    int32_t* clist_o = (int32_t*)(b + off_clo);
-    uint32_t* cbin_hist = (uint32_t*)(b + off_ct);
-    (void)cbin_hist; (void)clist_o;
     bool sorted = false;   // this step's lists are in lists_o
 #if PT_WF_BIN
     auto bin_sort = [&]() -> hipError_t {   // (the device reads the list's length: no host wait)
@@ -1297,24 +1280,8 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
         return times ? hipEventRecord(s->prof_ev[(size_t)step * kEv + k * 2 + end], on) : hipSuccess;
     };
     // step 0 walks the primary queries (CQP, one per pixel), later steps the slots' (CQ)
-#if PT_WF_CBIN && PT_WF_BIN
-    // (dev) the closest list counting-sorted by its origin's cell on the walk's stream
-    auto cbin_sort = [&](hipStream_t on) -> hipError_t {
-        uint32_t* h = cbin_hist;
-        uint32_t* rs = h + (size_t)kBins * kBinBlocks;
-        uint32_t* bs = rs + kBins;
-        const int32_t* cnt = counters + 2;
-        const int32_t* l = lists + 3 * slots;
-        hipLaunchKernelGGL(k_bin_hist, dim3(kBinBlocks), dim3(256), 0, on, (const uint16_t*)ckeys, cnt, h);
-        hipLaunchKernelGGL(k_bin_rows, dim3(kBins / 4), dim3(256), 0, on, h, cnt, rs);
-        hipLaunchKernelGGL(k_bin_base, dim3(1), dim3(1024), 0, on, (const uint32_t*)rs, bs);
-        hipLaunchKernelGGL(k_bin_scatter, dim3(kBinBlocks), dim3(256), 0, on, (const uint16_t*)ckeys, l, cnt,
-                           (const uint32_t*)h, (const uint32_t*)bs, clist_o);
-        return hipGetLastError();
-    };
-#endif
     auto closest_walk = [&](hipStream_t on, int32_t step) {
-        const int32_t* l = (PT_WF_CBIN && PT_WF_BIN && step > 0) ? clist_o : lists + 3 * slots;
+        const int32_t* l = lists + 3 * slots;
         WfClosestQ* q = step == 0 ? CQP : CQ;
         const uint32_t ws = step == 0 ? R.split_log2 : 0u;
         if (s->dev.bunitc) {
@@ -1341,7 +1308,7 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
         HIPCHK(mark(step, 0, 0, st));
         hipLaunchKernelGGL(k_wf_shade, dim3((unsigned)((slots + kShadeBlock - 1) / kShadeBlock)),
                            dim3(kShadeBlock), 0, st, s->dev, R, step, W, SQ, CQ,
-                           (const WfClosestQ*)CQP, lists, counters, (uint32_t)slots, keys, ckeys);
+                           (const WfClosestQ*)CQP, lists, counters, (uint32_t)slots, keys);
         if (step == 0)
             hipLaunchKernelGGL(k_wf_primary, dim3((R.npix + 255) / 256), dim3(256), 0, st, s->dev, R, W,
                                CQP, lists + 3 * slots, counters + 2);
@@ -1359,9 +1326,6 @@ static int render_wavefront(pt_scene* s, const RenderK& R, dim3 grid, void* out_
                 HIPCHK(hipEventRecord(s->wf_ev_shade, st));
                 HIPCHK(hipStreamWaitEvent(s->wf_side, s->wf_ev_shade, 0));
             }
-#if PT_WF_CBIN && PT_WF_BIN
-            if (step > 0) HIPCHK(cbin_sort(cs));
-#endif
             HIPCHK(mark(step, 2, 0, cs));
             closest_walk(cs, step);
             HIPCHK(mark(step, 2, 1, cs));

@@ -400,7 +400,7 @@ PT_HD QuadM quad_m(const UnitF& U, const RayPlane& p, const OriginU& O, F3 d) {
     return r;
 }
 #ifndef PT_MICRO
-#define PT_MICRO 6
+#define PT_MICRO 2
 #endif
 // origin terms of the render loop's unit form (the second member's only for
 // a pair that is no parallelogram), and (PT_VCONST) VGPR copies of the
@@ -482,19 +482,21 @@ PT_HD float pt_canon(float x) {
 #ifndef PT_DEL_PRE
 #define PT_DEL_PRE 0
 #endif
+#ifndef PT_VOTE_MIN3
+#define PT_VOTE_MIN3 0
+#endif
 PT_HD void margin_unit(float cm, float nm, float M, float del, float* c, float* a) {
     *c = nan_min(cm, M - del);
     *a = fminf(fminf(nm, M + del), -*c);
 }
 // fmaxf of two quiet-NaN-or-number values without the canonicalising
 // v_max_f32 x, x the compiler puts before an IEEE-mode v_max_f32 whose input
-// comes through a phi: v_med3_f32(a, b, +inf) is max(a, b), and with a NaN
-// input it returns v_min3_f32(a, b, +inf), i.e. the other operand (fmaxf's
-// result).  The values here come from arithmetic (quiet NaNs only).
+// comes through a phi: the instruction itself (IEEE maxNum: a quiet NaN
+// operand returns the other one, as fmaxf does).  The values here come from
+// arithmetic (quiet NaNs only).  (A v_med3_f32(a, b, FLT_MAX) form avoids the
+// asm's s_nop but costs an SGPR: 0.5% slower)
 PT_HD float fmax_q(float a, float b) {
-#if defined(__HIP_DEVICE_COMPILE__) && PT_FMAX_MED3
-    return __builtin_amdgcn_fmed3f(a, b, 3.40282347e38f);
-#elif defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
     float r;
     asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
@@ -1921,8 +1923,12 @@ PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& 
             for (int u = 0; u < S.n_obj_unit; ++u) {
                 const UnitF U = S.unit[u];
                 const OriginU O = PT_QUAD ? origin_q(U, o32u) : origin_u(U, o32u);
+#if PT_VOTE_MIN3   // (oc is never NaN: the three compares as one minimum)
+                const bool do_shadow = PT_WAVE_ANY(!(min3f(oc[0], oc[1], oc[2]) > 0.0f));
+#else
                 const bool do_shadow =
                     PT_WAVE_ANY(!(oc[0] > 0.0f && oc[1] > 0.0f && oc[2] > 0.0f));
+#endif
                 fused_unit<FORCE64, COUNT, true>(S, U, O, U.grp == ogrp, do_shadow, any_trace,
                                                  &sh, n32, &ca, sp, cnt, 15u, oc);
             }

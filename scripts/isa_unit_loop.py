@@ -47,12 +47,10 @@ def main():
     for i, l in enumerate(f):
         if "Inner Loop Header: Depth=2" in l:
             lab = (f[i] if f[i].startswith(".LBB") else f[i - 1]).split(":")[0]
-            body = "\n".join(f[i:i + 6])
-            if "s_load_dwordx8" in body or "s_load_dwordx16" in body:
-                nm = lab.replace(".LBB", "BB")
-                n = sum(1 for x in f if ("Header=" + nm) in x)
-                if n > size:
-                    best, size = lab, n
+            nm = lab.replace(".LBB", "BB")
+            n = sum(1 for x in f if ("Header=" + nm) in x)
+            if n > size:   # (the fused pass is by far the largest depth-2 loop)
+                best, size = lab, n
     if best is None:
         raise SystemExit("unit loop not found")
     name = best.replace(".LBB", "BB")
