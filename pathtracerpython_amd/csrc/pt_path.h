@@ -400,7 +400,7 @@ PT_HD QuadM quad_m(const UnitF& U, const RayPlane& p, const OriginU& O, F3 d) {
     return r;
 }
 #ifndef PT_MICRO
-#define PT_MICRO 2
+#define PT_MICRO 5
 #endif
 // origin terms of the render loop's unit form (the second member's only for
 // a pair that is no parallelogram), and (PT_VCONST) VGPR copies of the
@@ -480,10 +480,13 @@ PT_HD float pt_canon(float x) {
 #define PT_CLOSEST_LEAN 1
 #endif
 #ifndef PT_DEL_PRE
-#define PT_DEL_PRE 0
+#define PT_DEL_PRE 1
 #endif
 #ifndef PT_VOTE_MIN3
-#define PT_VOTE_MIN3 0
+#define PT_VOTE_MIN3 1
+#endif
+#ifndef PT_LIGHT_QUAD
+#define PT_LIGHT_QUAD 1
 #endif
 PT_HD void margin_unit(float cm, float nm, float M, float del, float* c, float* a) {
     *c = nan_min(cm, M - del);
@@ -687,6 +690,33 @@ PT_HD void fused_fallback(const SceneK& S, const UnitF& U, uint32_t amb, ShadowS
     }
 }
 
+// The next ray's closest-hit test against a uniform unit in the render
+// loop's unit form (quad_m): per-member verdicts as lane masks, the candidate
+// into ca, the ambiguous members as bits 6 / 7 of *amb.
+PT_HD void closest_unit_m(const UnitF& U, const OriginU& O, bool coplanar, F3 n32, ClosestAcc* ca,
+                          uint32_t* amb) {
+    RayPlane p = ray_plane_e(U, O.h, n32, INFINITY, INFINITY, O.eh, O.eo);
+#if PT_CLOSEST_LEAN
+    // the closest ray's range has no far end (hi_lo = hi_hi = inf): rcand's
+    // "at + dt < inf" follows from |q| > qhi (>= 1e-5: |t| <= |h| 1e5 (1 + u),
+    // dt finite, for the finite origins and records here), and rmiss's
+    // "at - dt >= inf" only holds for |t| = inf (q exactly 0), which is then
+    // ambiguous (del = inf) and decided in f64 — two compares less per unit,
+    // the same certain verdicts
+    p.rcand = (fabsf(p.q) > U.qhi) & (p.at - p.dt > kTzHi);
+    p.rmiss = p.at + p.dt < kTzLo;
+#endif
+    const QuadM m = quad_m(U, p, O, n32);
+    const Verdict v0 = verdict_m(m.m0, p), v1 = verdict_m(m.m1, p);
+    const bool c0 = v0.cand & !coplanar, a0 = v0.amb & !coplanar;
+    const bool c1 = v1.cand & !coplanar, a1 = v1.amb & !coplanar;
+    // both candidates of one unit cannot happen (a point certainly inside
+    // one triangle is certainly outside its coplanar neighbour)
+    const bool c = c0 | c1;
+    closest_add(ca, c0 ? U.t[0] : U.t[1], c ? p.at - p.dt : INFINITY, c ? p.at + p.dt : INFINITY);
+    *amb |= (a0 ? 64u : 0u) | (a1 ? 128u : 0u);
+}
+
 // One plane unit against the 3 shadow rays and the next ray's closest hit,
 // all from the same origin (the fused per-bounce pass).  Every verdict is
 // computed branch-free; ambiguous tests are only recorded as bits and
@@ -752,44 +782,26 @@ PT_HD void fused_unit(const SceneK& S, const UnitF& U, const OriginU& O, bool co
         }
     }
     if (!FORCE64 && do_closest && (rays & 8u)) {
-        RayPlane p = (MARGIN && PT_QUAD) ? ray_plane_e(U, O.h, n32, INFINITY, INFINITY, O.eh, O.eo)
-                                         : ray_plane(U, O.h, n32, INFINITY, INFINITY);
-#if PT_CLOSEST_LEAN
-        if (MARGIN && PT_QUAD) {
-            // the closest ray's range has no far end (hi_lo = hi_hi = inf):
-            // rcand's "at + dt < inf" follows from |q| > qhi (>= 1e-5: |t| <=
-            // |h| 1e5 (1 + u), dt finite, for the finite origins and records
-            // here), and rmiss's "at - dt >= inf" only holds for |t| = inf (q
-            // exactly 0), which is then ambiguous (del = inf) and decided in
-            // f64 — two compares less per unit, the same certain verdicts
-            p.rcand = (fabsf(p.q) > U.qhi) & (p.at - p.dt > kTzHi);
-            p.rmiss = p.at + p.dt < kTzLo;
-        }
-#endif
-        bool c0, a0, c1 = false, a1 = false;
         if (MARGIN && PT_QUAD) {   // the render loop's unit form (quad_m)
-            const QuadM m = quad_m(U, p, O, n32);
-            const Verdict v0 = verdict_m(m.m0, p), v1 = verdict_m(m.m1, p);
-            c0 = v0.cand & !coplanar;
-            a0 = v0.amb & !coplanar;
-            c1 = v1.cand & !coplanar;
-            a1 = v1.amb & !coplanar;
+            closest_unit_m(U, O, coplanar, n32, ca, &amb);
         } else {
+            const RayPlane p = ray_plane(U, O.h, n32, INFINITY, INFINITY);
+            bool c1 = false, a1 = false;
             const Verdict v0 = classify_tri(U.tri[0], p, O.bo0, O.co0, n32);
-            c0 = v0.cand & !coplanar;
-            a0 = v0.amb & !coplanar;
+            const bool c0 = v0.cand & !coplanar;
+            const bool a0 = v0.amb & !coplanar;
             if (two) {
                 const Verdict v1 = classify_tri(U.tri[1], p, O.bo1, O.co1, n32);
                 c1 = v1.cand & !coplanar;
                 a1 = v1.amb & !coplanar;
             }
+            // both candidates of one unit cannot happen (a point certainly inside
+            // one triangle is certainly outside its coplanar neighbour)
+            const bool c = c0 | c1;
+            closest_add(ca, c0 ? U.t[0] : U.t[1], c ? p.at - p.dt : INFINITY,
+                        c ? p.at + p.dt : INFINITY);
+            amb |= (a0 ? 64u : 0u) | (a1 ? 128u : 0u);
         }
-        // both candidates of one unit cannot happen (a point certainly inside
-        // one triangle is certainly outside its coplanar neighbour)
-        const bool c = c0 | c1;
-        closest_add(ca, c0 ? U.t[0] : U.t[1], c ? p.at - p.dt : INFINITY,
-                    c ? p.at + p.dt : INFINITY);
-        amb |= (a0 ? 64u : 0u) | (a1 ? 128u : 0u);
     }
     if (PT_AMB_MAX && MARGIN && PT_QUAD && (PARTS & 1) && !(amax < 0.0f))   // rare: rebuild the bits
         amb |= shadow_bits_m(S, U, O, coplanar, sh, oc);
@@ -1959,6 +1971,14 @@ PT_HD void render_loop(const SceneK& S, const LaneJob& J, int tri, const Spill& 
         if (!FORCE64 && any_trace) {
             for (int u = S.n_obj_unit; u < S.n_unit; ++u) {   // the light's units
                 const UnitF U = S.unit[u];
+#if PT_LIGHT_QUAD && PT_QUAD && PT_MARGIN
+                if (!COUNT) {   // the render loop's unit form (one pair of forms for a quad)
+                    uint32_t amb = 0;
+                    closest_unit_m(U, origin_q(U, o32u), U.grp == ogrp, n32, &ca, &amb);
+                    if (amb) fused_fallback<FORCE64, COUNT, true, 2>(S, U, amb, &sh, &ca, sp, cnt, nullptr);   // rare
+                    continue;
+                }
+#endif
                 closest_unit<COUNT>(S, U, origin_u(U, o32u), n32, U.grp == ogrp, sp, kSpP, kSpNd,
                                     &ca, cnt);
             }
