@@ -1124,6 +1124,12 @@ static int validate(const pt_render_params* p) {
 // framebuffer stays bitwise equal to the wavefront one.
 //
 // PT_SPLIT_FIXED (compile-time, tuning builds only) pins the split.
+// PT_MIN_SPL: samples per lane the whole-image split keeps at least (round 6:
+// 4, i.e. 16 lanes per pixel at K2 — 4.669-4.693 vs 4.741-4.744 ms at 8 samples
+// per lane; round 5's kernel was flat between 8 and 16 lanes)
+#ifndef PT_MIN_SPL
+#define PT_MIN_SPL 4
+#endif
 static uint32_t choose_split(uint64_t image_pixels, uint64_t launch_pixels, int32_t spp, bool bvh,
                              uint64_t min_lanes) {
     uint32_t cap = 64;
@@ -1136,7 +1142,7 @@ static uint32_t choose_split(uint64_t image_pixels, uint64_t launch_pixels, int3
 #else
     uint32_t s = 1;
     const uint64_t target = (uint64_t)1 << (bvh ? 26 : 30);
-    while (s < cap && image_pixels * s * 2 <= target && (bvh || spp / (int32_t)(s * 2) >= 8)) s *= 2;
+    while (s < cap && image_pixels * s * 2 <= target && (bvh || spp / (int32_t)(s * 2) >= PT_MIN_SPL)) s *= 2;
     if (!bvh)
         while (s < cap && launch_pixels * s < min_lanes) s *= 2;
     return s;

@@ -68,6 +68,9 @@ constexpr int kSpillSlots = 20;
 #ifndef PT_WF_LRNG
 #define PT_WF_LRNG 1
 #endif
+#ifndef PT_SETUP_REUSE
+#define PT_SETUP_REUSE 1
+#endif
 // P and Nd first: the wavefront path record (pt_wavefront.h WfPath) keeps them
 // in the same 128-B line as the per-step fields; the light points and the
 // primary hit follow in the other line
@@ -271,8 +274,18 @@ PT_HD void shadow_setup_k(const SceneK& S, D3 P, D3 n, int k, double u0, double 
     const int li = pick_light(S, u0);
     const D3 L = light_point(S.trid[S.light_tri[li]], u1, u2, u3);
     if (STORE_L) sp.put3(kSpL + 3 * k, L);
+#if PT_SETUP_REUSE
+    // |L - P|^2 once: squared_dist(P, L) sums the same squares in the same
+    // order as unit()'s dot (dx = P - L only flips the signs the squares drop,
+    // and 0 + x^2 is x^2), so both uses get the same bits
+    const D3 a = L - P;
+    const double s2 = dot(a, a);
+    const D3 dn = a * rsqrt_d(s2);                // main.py:37-38 (unit())
+    const float tl = sqrtf((float)s2);            // main.py:40, to ~2e-7
+#else
     const D3 dn = unit(L - P);                    // main.py:37-38
     const float tl = sqrtf((float)squared_dist(P, L));   // main.py:40, to ~2e-7
+#endif
     sh->hlo[k] = tl * (1.0f - 1e-6f);
     sh->hhi[k] = tl * (1.0f + 1e-6f);
     sh->d32[k] = to_f3(dn);
@@ -488,6 +501,9 @@ PT_HD float pt_canon(float x) {
 #ifndef PT_LIGHT_QUAD
 #define PT_LIGHT_QUAD 1
 #endif
+#ifndef PT_CADD_BF
+#define PT_CADD_BF 1
+#endif
 PT_HD void margin_unit(float cm, float nm, float M, float del, float* c, float* a) {
     *c = nan_min(cm, M - del);
     *a = fminf(fminf(nm, M + del), -*c);
@@ -505,6 +521,15 @@ PT_HD float fmax_q(float a, float b) {
     return r;
 #else
     return fmaxf(a, b);
+#endif
+}
+PT_HD float fmin_q(float a, float b) {   // fminf likewise (IEEE minNum of quiet NaNs or numbers)
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fminf(a, b);
 #endif
 }
 // nan_min(nan_min(a, b), c) as one v_minimum3_f32 (the compiler emits each
@@ -713,7 +738,19 @@ PT_HD void closest_unit_m(const UnitF& U, const OriginU& O, bool coplanar, F3 n3
     // both candidates of one unit cannot happen (a point certainly inside
     // one triangle is certainly outside its coplanar neighbour)
     const bool c = c0 | c1;
+#if PT_CADD_BF
+    // closest_add branch-free, the running minimum as an asm v_min_f32 (no
+    // canonicalising v_max x, x of its phi inputs; a and a2 are never NaN)
+    const float a = c ? p.at - p.dt : INFINITY, b = c ? p.at + p.dt : INFINITY;
+    const int tc = c0 ? U.t[0] : U.t[1];
+    const bool lt = a < ca->a1;
+    ca->a2 = lt ? ca->a1 : fmin_q(ca->a2, a);
+    ca->a1 = lt ? a : ca->a1;
+    ca->b1 = lt ? b : ca->b1;
+    ca->i1 = lt ? tc : ca->i1;
+#else
     closest_add(ca, c0 ? U.t[0] : U.t[1], c ? p.at - p.dt : INFINITY, c ? p.at + p.dt : INFINITY);
+#endif
     *amb |= (a0 ? 64u : 0u) | (a1 ? 128u : 0u);
 }
 

@@ -7,7 +7,7 @@ depth-2 loop that loads the 128-B unit records), and prints every basic block
 of the loop with its VALU / SALU / SMEM counts, marking the rare blocks (f64:
 the fallbacks and the shadow-bit rebuild).  --listing prints the hot blocks'
 instructions.
-    python3 scripts/isa_unit_loop.py [--listing] [-DNAME=VALUE ...]"""
+    python3 scripts/isa_unit_loop.py [--listing] [--csrc DIR] [-DNAME=VALUE ...]"""
 import collections
 import os
 import subprocess
@@ -21,11 +21,11 @@ from pathtracerpython_amd import build  # noqa: E402
 KERNEL = "_Z8k_renderILb0ELb0ELb0EE"
 
 
-def compile_asm(defines):
+def compile_asm(defines, csrc=build.CSRC):
     out = os.path.join(tempfile.gettempdir(), "pt_isa_%d.s" % os.getpid())
     cmd = [build.HIPCC, "--offload-arch=" + build.ARCH, "-O3", "-std=c++17", "-ffp-contract=off",
            "--cuda-device-only", "-S", "-DPT_BUILD_ID=\"isa\"", "-o", out] + defines + \
-          [os.path.join(build.CSRC, "pt_hip.hip")]
+          [os.path.join(csrc, "pt_hip.hip")]
     subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
     with open(out) as f:
         return f.read().split("\n")
@@ -34,7 +34,9 @@ def compile_asm(defines):
 def main():
     listing = "--listing" in sys.argv
     defines = [a for a in sys.argv[1:] if a.startswith("-D")]
-    s = compile_asm(defines)
+    # --csrc DIR: another source tree (e.g. an earlier round's, from git archive)
+    csrc = sys.argv[sys.argv.index("--csrc") + 1] if "--csrc" in sys.argv else build.CSRC
+    s = compile_asm(defines, csrc)
     start = next(i for i, l in enumerate(s) if l.startswith(KERNEL))
     end = next(i for i in range(start, len(s)) if s[i].startswith(".Lfunc_end"))
     f = s[start:end]

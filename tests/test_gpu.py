@@ -228,8 +228,8 @@ def test_interleaved_bands_assemble(R):
 
 def test_tail_rows_ragged(R, packed):
     """The single kernel's last rows run at 8x lanes per pixel (launch drain,
-    DESIGN.md §4).  999 x 300 at 64 spp runs 8 lanes per pixel, and the tail
-    (rows iy >= 281) starts at lane 281 x 999 x 8 = 2,245,752, padded to a wave
+    DESIGN.md §4).  999 x 300 at 64 spp runs 16 lanes per pixel, and the tail
+    (rows iy >= 281) starts at lane 281 x 999 x 16 = 4,491,504, padded to a wave
     boundary: rows below, at and above the threshold vs the oracle; a 3-way
     interleaved split (99,900 pixels per band: 16 lanes per pixel, their own
     tails) assembles to within rounding of the full frame."""
@@ -564,8 +564,11 @@ def test_render_multi_lanes_contract(cornell):
     with Renderer(cornell) as r:
         ref = r.render(W, H, 64, 4, 9, out_f64=True)
         ref8 = r.render_params(r.params(W, H, 64, 4, 9, out_f64=True, lanes_per_pixel=8))
+        ref16 = r.render_params(r.params(W, H, 64, 4, 9, out_f64=True, lanes_per_pixel=16))
         ref32 = r.render_params(r.params(W, H, 64, 4, 9, out_f64=True, lanes_per_pixel=32))
-    assert np.array_equal(ref8, ref)   # the whole K2 frame picks 8 lanes per pixel itself
+    # the whole K2 frame picks 16 lanes per pixel itself (4 samples per lane, round 6)
+    assert np.array_equal(ref16, ref)
+    assert np.abs(ref8 - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
     with MultiRenderer(cornell, [0] * 8) as m:
         auto = m.render(W, H, 64, 4, 9, out_f64=True)
         assert np.abs(auto - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
