@@ -31,3 +31,11 @@ if "--times" in sys.argv:   # each kernel's own time (the walks one after the ot
     print("own ms per render: shade %.1f shadow %.1f closest %.1f sort %.1f (launches %d / %d / %d / %d)" % (
         kt["shade_ms"], kt["shadow_ms"], kt["closest_ms"], kt["sort_ms"], kt["shade_launches"],
         kt["shadow_launches"], kt["closest_launches"], kt["sort_launches"]))
+if "--counts" in sys.argv:   # the walks' work (PT_FLAG_WALK_COUNT launch)
+    from pathtracerpython_amd._abi import PT_FLAG_WALK_COUNT, with_flags
+    _, wc = r.render_params(with_flags(p, PT_FLAG_WALK_COUNT), stats=True)
+    for k in ("shadow", "closest"):
+        q = max(1, wc[k + "_queries"])
+        print("%s walks: queries %d, node visits %d (%.2f per query), leaf units %d (%.2f per query)" % (
+            k, wc[k + "_queries"], wc[k + "_node_visits"], wc[k + "_node_visits"] / q,
+            wc[k + "_leaf_units"], wc[k + "_leaf_units"] / q))
