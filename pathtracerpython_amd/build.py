@@ -18,12 +18,15 @@ ROOT = os.path.dirname(HERE)
 HEADER = os.path.join(ROOT, "include", "pt_capi.h")
 OUT = os.path.join(HERE, "_lib", "libpt_hip.so")
 SOURCES = ["pt_hip.hip"]
+# translation units compiled on their own, with extra code-generation flags,
+# and linked into the library: the K2 kernel under LLVM's iterative ILP
+# scheduler (pt_k2.hip; the walk kernels lose under it)
+UNITS = {"pt_k2.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # -ffp-contract=off: every f64 operation rounds separately, as the reference's
 # numpy does; the f32 filter writes its fmaf() explicitly.
-FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-         "-ffp-contract=off", "-Wall"]
+FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
 # the id string in the library: MARKER followed by the 16 hex digits
 MARKER = b"PT_BUILD_ID="
 ID_LEN = 16
@@ -75,16 +78,26 @@ def variant_id(sha, defines):
 
 def compile_lib(out, defines=(), csrc=CSRC, verbose=True):
     """hipcc the library into `out`, stamped with the hash of `csrc`'s sources
-    (dev variants pass -D switches: their id also covers the switches,
+    (dev variants pass -D switches or raw flags: their id also covers them,
     variant_id)."""
     sha = variant_id(source_sha(csrc), tuple(defines))
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = ([HIPCC] + FLAGS + [f"-DPT_BUILD_ID=\"{sha}\""] + ["-D" + d for d in defines] +
-           ["-o", out + ".tmp"] +
-           [os.path.join(csrc, s) for s in SOURCES])
+    # (an item starting with "-" is a raw compiler flag, e.g. -mllvm options)
+    common = FLAGS + [f"-DPT_BUILD_ID=\"{sha}\""] + [d if d.startswith("-") else "-D" + d for d in defines]
+    objs = []
+    for unit, extra in [(u, []) for u in SOURCES] + list(UNITS.items()):
+        obj = "%s.%s.o" % (out, os.path.splitext(unit)[0])
+        cmd = [HIPCC] + common + extra + ["-c", "-o", obj, os.path.join(csrc, unit)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-fPIC", "-shared", "--hip-link", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    for obj in objs:
+        os.remove(obj)
     os.replace(out + ".tmp", out)
     return out
 

@@ -23,9 +23,12 @@ KERNEL = "_Z8k_renderILb0ELb0ELb0EE"
 
 def compile_asm(defines, csrc=build.CSRC):
     out = os.path.join(tempfile.gettempdir(), "pt_isa_%d.s" % os.getpid())
+    # the K2 kernel's translation unit and its flags (build.UNITS), when the
+    # tree has one (an earlier round's, --csrc: pt_hip.hip)
+    unit = "pt_k2.hip" if os.path.exists(os.path.join(csrc, "pt_k2.hip")) else "pt_hip.hip"
     cmd = [build.HIPCC, "--offload-arch=" + build.ARCH, "-O3", "-std=c++17", "-ffp-contract=off",
-           "--cuda-device-only", "-S", "-DPT_BUILD_ID=\"isa\"", "-o", out] + defines + \
-          [os.path.join(csrc, "pt_hip.hip")]
+           "--cuda-device-only", "-S", "-DPT_BUILD_ID=\"isa\"", "-o", out] + \
+          build.UNITS.get(unit, []) + defines + [os.path.join(csrc, unit)]
     subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
     with open(out) as f:
         return f.read().split("\n")
@@ -33,7 +36,7 @@ def compile_asm(defines, csrc=build.CSRC):
 
 def main():
     listing = "--listing" in sys.argv
-    defines = [a for a in sys.argv[1:] if a.startswith("-D")]
+    defines = [a for a in sys.argv[1:] if a.startswith("-") and a not in ("--listing", "--csrc")]
     # --csrc DIR: another source tree (e.g. an earlier round's, from git archive)
     csrc = sys.argv[sys.argv.index("--csrc") + 1] if "--csrc" in sys.argv else build.CSRC
     s = compile_asm(defines, csrc)
