@@ -19,9 +19,11 @@ HEADER = os.path.join(ROOT, "include", "pt_capi.h")
 OUT = os.path.join(HERE, "_lib", "libpt_hip.so")
 SOURCES = ["pt_hip.hip"]
 # translation units compiled on their own, with extra code-generation flags,
-# and linked into the library: the K2 kernel under LLVM's iterative ILP
-# scheduler (pt_k2.hip; the walk kernels lose under it)
-UNITS = {"pt_k2.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]}
+# and linked into the library: the K2 kernel (pt_k2.hip) and the wavefront
+# shade step (pt_shade.hip) under LLVM's iterative ILP scheduler (the walk
+# kernels lose under it)
+_ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+UNITS = {"pt_k2.hip": _ILP, "pt_shade.hip": _ILP}
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # -ffp-contract=off: every f64 operation rounds separately, as the reference's
@@ -85,7 +87,11 @@ def compile_lib(out, defines=(), csrc=CSRC, verbose=True):
     # (an item starting with "-" is a raw compiler flag, e.g. -mllvm options)
     common = FLAGS + [f"-DPT_BUILD_ID=\"{sha}\""] + [d if d.startswith("-") else "-D" + d for d in defines]
     objs = []
+    # (a variant's own scheduler strategy replaces a unit's)
+    own_sched = any(d.startswith("-amdgpu-sched-strategy") for d in defines)
     for unit, extra in [(u, []) for u in SOURCES] + list(UNITS.items()):
+        if own_sched:
+            extra = []
         obj = "%s.%s.o" % (out, os.path.splitext(unit)[0])
         cmd = [HIPCC] + common + extra + ["-c", "-o", obj, os.path.join(csrc, unit)]
         if verbose:
