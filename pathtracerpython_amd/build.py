@@ -2,7 +2,8 @@
 library travels with the repository snapshot to the GPU box).
 
 Every build is stamped with the content hash of the sources it was compiled
-from (`source_sha`: csrc/*.h, csrc/*.hip, include/pt_capi.h), compiled in as
+from (`source_sha`: csrc/*.h, csrc/*.hip, include/pt_capi.h, and the compile
+recipe: FLAGS and each unit's own flags, UNITS), compiled in as
 PT_BUILD_ID and exported by `pt_build_id()`.  Staleness is decided by that
 hash, not by file times, and `_native.lib()` refuses a library whose id is not
 the hash of the sources on disk, so a measurement always names the sources of
@@ -39,12 +40,22 @@ def source_files(csrc=CSRC, header=HEADER):
             if f.endswith((".h", ".hip"))] + [header]
 
 
-def source_sha(csrc=CSRC, header=HEADER):
-    """Content hash of the kernel sources (16 hex digits)."""
+def recipe(flags=None, units=None):
+    """The compile recipe as text: the common flags and each unit's own (the
+    same sources under other code-generation flags are another binary)."""
+    flags = FLAGS if flags is None else flags
+    units = UNITS if units is None else units
+    return "\0".join([ARCH] + list(flags) + ["%s:%s" % (u, " ".join(units[u])) for u in sorted(units)])
+
+
+def source_sha(csrc=CSRC, header=HEADER, flags=None, units=None):
+    """Content hash of the kernel sources and the compile recipe (16 hex
+    digits)."""
     h = hashlib.sha256()
     for p in source_files(csrc, header):
         with open(p, "rb") as f:
             h.update(f.read())
+    h.update(recipe(flags, units).encode())
     return h.hexdigest()[:ID_LEN]
 
 

@@ -214,6 +214,18 @@ def test_build_is_stale_when_a_source_changes(tmp_path):
     assert build._stale(csrc=str(csrc))
 
 
+def test_build_id_covers_the_compile_recipe():
+    """The K2 kernel's and the shade step's units are compiled under their own
+    scheduler flag (build.UNITS): the same sources under another recipe are
+    another binary, so they carry another id."""
+    from pathtracerpython_amd import build
+    assert set(build.UNITS) == {"pt_k2.hip", "pt_shade.hip"}
+    for u in build.UNITS:
+        assert os.path.exists(os.path.join(build.CSRC, u))
+    assert build.source_sha(units={}) != build.source_sha()
+    assert build.source_sha(flags=build.FLAGS + ["-O2"]) != build.source_sha()
+
+
 def test_variant_builds_carry_their_own_id():
     """a build with -D switches is named by the sources AND its
     switches, so it never passes for the default build (the binding loads it
