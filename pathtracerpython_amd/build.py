@@ -95,12 +95,21 @@ def compile_lib(out, defines=(), csrc=CSRC, verbose=True):
     variant_id)."""
     sha = variant_id(source_sha(csrc), tuple(defines))
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    # (an item starting with "-" is a raw compiler flag, e.g. -mllvm options)
+    # (an item starting with "-" is a raw compiler flag, e.g. -mllvm options;
+    # "UNIT=name.hip:flags ..." replaces that unit's own flags)
+    unit_flags = dict(UNITS)
+    for d in defines:
+        if d.startswith("UNIT="):
+            name, _, fl = d[5:].partition(":")
+            if name not in UNITS:
+                raise ValueError("UNIT= names one of %s" % sorted(UNITS))
+            unit_flags[name] = fl.split()
+    defines = [d for d in defines if not d.startswith("UNIT=")]
     common = FLAGS + [f"-DPT_BUILD_ID=\"{sha}\""] + [d if d.startswith("-") else "-D" + d for d in defines]
     objs = []
     # (a variant's own scheduler strategy replaces a unit's)
     own_sched = any(d.startswith("-amdgpu-sched-strategy") for d in defines)
-    for unit, extra in [(u, []) for u in SOURCES] + list(UNITS.items()):
+    for unit, extra in [(u, []) for u in SOURCES] + list(unit_flags.items()):
         if own_sched:
             extra = []
         obj = "%s.%s.o" % (out, os.path.splitext(unit)[0])

@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 6, call q: the shade step's scheduler (variants sh_*: max-memory-clause,
+# max-ilp, the default, against the built library's iterative-ilp) on the K5 proxy
+# and at full size
+set -euo pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out/r06q
+ROUNDS=2 LIMIT=120 bash scripts/variants.sh sh_ python3 scripts/prof_k5.py 3 512 64 --times 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r06q/k5.txt
+ROUNDS=1 LIMIT=200 bash scripts/variants.sh sh_ python3 scripts/prof_k5.py 2 1024 256 --times 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r06q/k5_full.txt
